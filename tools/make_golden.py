@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by importing the REFERENCE (this container only).
+
+Runs the reference's own code from ``/root/reference/acestep/models/{base,turbo}``
+(read-only, never copied) on small inputs and stores inputs + outputs as
+safetensors fixtures under ``tests/golden/``.  Weights are NOT stored: they
+are regenerated bit-exactly from ``acehip.weights.synth_dit_weights(cfg,
+seed, mode="parity")`` (NumPy PCG64), and a checksum is stored to detect drift.
+
+Fixtures:
+  dit_fwd_*.safetensors      one decoder forward (tiny + full-width configs,
+                             fp32 + bf16, even/odd T)
+  temb_*.safetensors         TimestepEmbedding outputs for schedule values
+  sampler_*.safetensors      a whole generate_audio (base CFG+APG / turbo)
+                             driven by a deterministic stand-in decoder that
+                             records every (x, t, vt) — pins schedules, APG,
+                             momentum, Euler/x0 arithmetic bit-exactly.
+
+``vector_quantize_pytorch`` (absent here) is stubbed; its ResidualFSQ is only
+used by the audio tokenizer whose output is discarded when is_covers=0
+(reference base:1645-1649).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import torch
+from safetensors.torch import save_file
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ace-step-1.5_amd"))
+OUT = os.path.join(REPO, "tests", "golden")
+
+from acehip.config import DiTConfig  # noqa: E402
+from acehip.weights import synth_dit_weights, synth_null_condition  # noqa: E402
+
+
+def _stub_vq():
+    m = types.ModuleType("vector_quantize_pytorch")
+
+    class ResidualFSQ(torch.nn.Module):
+        def __init__(self, *a, **k):
+            super().__init__()
+
+        def forward(self, x):
+            return x, None
+
+    m.ResidualFSQ = ResidualFSQ
+    sys.modules["vector_quantize_pytorch"] = m
+
+
+def _import_ref(variant: str):
+    _stub_vq()
+    d = f"/root/reference/acestep/models/{variant}"
+    for k in list(sys.modules):
+        if k.startswith(("configuration_acestep_v15", "modeling_acestep_v15", "apg_guidance")):
+            del sys.modules[k]
+    sys.path.insert(0, d)
+    try:
+        import configuration_acestep_v15 as C
+        mod = __import__(f"modeling_acestep_v15_{variant}")
+    finally:
+        sys.path.remove(d)
+    return C, mod
+
+
+def ref_config(C, cfg: DiTConfig, **extra):
+    rc = C.AceStepConfig(hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+                         num_hidden_layers=cfg.num_hidden_layers,
+                         num_attention_heads=cfg.num_attention_heads,
+                         num_key_value_heads=cfg.num_key_value_heads, head_dim=cfg.head_dim,
+                         sliding_window=cfg.sliding_window, **extra)
+    rc._attn_implementation = "sdpa"
+    return rc
+
+
+def checksum(W) -> float:
+    return float(sum(float(v.double().abs().sum()) for v in W.values()))
+
+
+def gen_forward(M, C, name, cfg: DiTConfig, B, T, Lenc, dtype, seed, t_vals, tr_vals):
+    rc = ref_config(C, cfg)
+    model = M.AceStepDiTModel(rc).eval()
+    W = synth_dit_weights(cfg, seed=seed, mode="parity")
+    missing, unexpected = model.load_state_dict(W, strict=False)
+    assert not unexpected and all("rotary" in k for k in missing), (missing, unexpected)
+    model = model.to(dtype)
+    g = torch.Generator().manual_seed(1234 + T)
+    xt = torch.randn(B, T, 64, generator=g).to(dtype)
+    ctx = torch.randn(B, T, 128, generator=g).to(dtype)
+    ctx[..., 64:] = (ctx[..., 64:] > 0).to(dtype)  # chunk-mask-like channels
+    enc = torch.randn(B, Lenc, cfg.hidden_size, generator=g).to(dtype)
+    t = torch.tensor(t_vals, dtype=dtype)
+    tr = torch.tensor(tr_vals, dtype=dtype)
+    with torch.no_grad():
+        out = model(hidden_states=xt, timestep=t, timestep_r=tr, attention_mask=None,
+                    encoder_hidden_states=enc, encoder_attention_mask=None,
+                    context_latents=ctx, use_cache=False)[0]
+    save_file({"xt": xt, "ctx": ctx, "enc": enc, "t": t, "t_r": tr, "vt": out.contiguous()},
+              os.path.join(OUT, f"dit_fwd_{name}.safetensors"))
+    return {"cfg": cfg.__dict__, "B": B, "T": T, "Lenc": Lenc, "dtype": str(dtype),
+            "seed": seed, "weights_checksum": checksum(W)}
+
+
+def gen_temb(M, C, cfg, dtype, seed):
+    rc = ref_config(C, cfg)
+    model = M.AceStepDiTModel(rc).eval()
+    model.load_state_dict(synth_dit_weights(cfg, seed=seed, mode="parity"), strict=False)
+    model = model.to(dtype)
+    t = torch.tensor([1.0, 0.9545454545454546, 0.75, 0.5, 0.3, 0.125, 0.0], dtype=dtype)
+    with torch.no_grad():
+        temb, proj = model.time_embed(t)
+    save_file({"t": t, "temb": temb.contiguous(), "proj": proj.contiguous()},
+              os.path.join(OUT, f"temb_{str(dtype).split('.')[-1]}.safetensors"))
+
+
+class _Recorder(torch.nn.Module):
+    """Stand-in decoder: deterministic, depends on x, t, encoder states and
+    context so cond/uncond halves differ; records every call."""
+
+    def __init__(self):
+        super().__init__()
+        self.calls = []
+
+    def forward(self, hidden_states, timestep, timestep_r, attention_mask, encoder_hidden_states,
+                encoder_attention_mask, context_latents, use_cache=True, past_key_values=None, **kw):
+        x = hidden_states
+        e = torch.tanh(encoder_hidden_states.float().mean(1, keepdim=True)[..., :64])
+        v = (0.6 * x.float() + 0.4 * e + 0.1 * context_latents[..., :64].float()
+             * timestep.float()[:, None, None] + 0.05 * torch.sin(3.0 * x.float()))
+        v = v.to(x.dtype)
+        self.calls.append((x.clone(), timestep.clone(), v.clone(), encoder_hidden_states.clone(),
+                           context_latents.clone()))
+        return (v, past_key_values)
+
+
+def gen_sampler(variant, name, dtype, B, T, **gen_kw):
+    C, M = _import_ref(variant)
+    cfg = DiTConfig.tiny(layers=1)
+    rc = ref_config(C, cfg, num_lyric_encoder_hidden_layers=1, num_timbre_encoder_hidden_layers=1,
+                    num_attention_pooler_hidden_layers=1, num_audio_decoder_hidden_layers=1)
+    torch.manual_seed(0)
+    model = M.AceStepConditionGenerationModel(rc).eval().to(dtype)
+    with torch.no_grad():
+        model.null_condition_emb.copy_(synth_null_condition(cfg, seed=7).to(dtype))
+    rec = _Recorder()
+    model.decoder = rec
+    g = torch.Generator().manual_seed(99)
+    Lt, Ll = 6, 9
+    kw = dict(
+        text_hidden_states=torch.randn(B, Lt, 1024, generator=g).to(dtype),
+        text_attention_mask=torch.ones(B, Lt, dtype=torch.long),
+        lyric_hidden_states=torch.randn(B, Ll, 1024, generator=g).to(dtype),
+        lyric_attention_mask=torch.ones(B, Ll, dtype=torch.long),
+        refer_audio_acoustic_hidden_states_packed=torch.randn(B, 750, 64, generator=g).to(dtype),
+        refer_audio_order_mask=torch.arange(B, dtype=torch.long),
+        src_latents=torch.randn(B, T, 64, generator=g).to(dtype),
+        chunk_masks=torch.ones(B, T, 64, dtype=dtype),
+        is_covers=torch.zeros(B, dtype=torch.long),
+        silence_latent=torch.randn(1, T, 64, generator=g).to(dtype),
+        seed=list(range(B)), use_progress_bar=False,
+    )
+    kw.update(gen_kw)
+    with torch.no_grad():
+        res = model.generate_audio(**kw)
+    tensors = {"target_latents": res["target_latents"].contiguous()}
+    for i, (x, t, v, e, c) in enumerate(rec.calls):
+        tensors[f"x_{i}"] = x
+        tensors[f"t_{i}"] = t
+        tensors[f"vt_{i}"] = v
+    tensors["enc"] = rec.calls[0][3]
+    tensors["ctx"] = rec.calls[0][4]
+    save_file(tensors, os.path.join(OUT, f"sampler_{name}.safetensors"))
+    meta = {k: (v if isinstance(v, (int, float, str, bool, list)) else None) for k, v in gen_kw.items()}
+    return {"variant": variant, "dtype": str(dtype), "B": B, "T": T, "n_calls": len(rec.calls),
+            "kwargs": meta}
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(8)
+    manifest = {"generator": "tools/make_golden.py", "reference": "/root/reference (read-only import)",
+                "torch": torch.__version__}
+    import transformers
+    manifest["transformers"] = transformers.__version__
+    C, M = _import_ref("base")
+    fw = {}
+    tiny = DiTConfig.tiny(layers=4, window=8)
+    for dt in (torch.float32, torch.bfloat16):
+        tag = str(dt).split(".")[-1]
+        fw[f"tiny_{tag}"] = gen_forward(M, C, f"tiny_{tag}", tiny, 2, 50, 20, dt, 11,
+                                        [0.75, 0.3], [0.75, 0.3])
+        fw[f"tiny_odd_{tag}"] = gen_forward(M, C, f"tiny_odd_{tag}", tiny, 2, 49, 13, dt, 12,
+                                            [1.0, 0.5], [0.25, 0.5])
+        gen_temb(M, C, tiny, dt, 11)
+    full2 = DiTConfig(num_hidden_layers=2)
+    for dt in (torch.float32, torch.bfloat16):
+        tag = str(dt).split(".")[-1]
+        fw[f"full2_{tag}"] = gen_forward(M, C, f"full2_{tag}", full2, 2, 64, 16, dt, 21,
+                                         [0.9, 0.9], [0.9, 0.9])
+    manifest["forward"] = fw
+    sm = {}
+    bf = torch.bfloat16
+    sm["base_s8_sh3"] = gen_sampler("base", "base_s8_sh3", bf, 2, 40, infer_steps=8, shift=3.0,
+                                    diffusion_guidance_sale=7.0)
+    sm["base_s27_sh3"] = gen_sampler("base", "base_s27_sh3", bf, 1, 40, infer_steps=27, shift=3.0,
+                                     diffusion_guidance_sale=7.0)
+    sm["base_s60_sh3"] = gen_sampler("base", "base_s60_sh3", bf, 1, 24, infer_steps=60, shift=3.0,
+                                     diffusion_guidance_sale=7.0)
+    sm["base_s10_sh1_interval"] = gen_sampler("base", "base_s10_sh1_interval", bf, 2, 32,
+                                              infer_steps=10, shift=1.0, diffusion_guidance_sale=4.0,
+                                              cfg_interval_start=0.3, cfg_interval_end=0.8)
+    sm["base_s8_nocfg_fp32"] = gen_sampler("base", "base_s8_nocfg_fp32", torch.float32, 2, 32,
+                                           infer_steps=8, shift=2.0, diffusion_guidance_sale=1.0)
+    sm["turbo_sh3"] = gen_sampler("turbo", "turbo_sh3", bf, 2, 40, shift=3.0)
+    sm["turbo_sh2"] = gen_sampler("turbo", "turbo_sh2", bf, 1, 40, shift=2.2)
+    sm["turbo_custom"] = gen_sampler("turbo", "turbo_custom", bf, 1, 40,
+                                     timesteps=torch.tensor([0.97, 0.76, 0.5, 0.26, 0.0]))
+    manifest["sampler"] = sm
+    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, default=str)
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()
