@@ -1,0 +1,117 @@
+"""ctypes binding of libacehip.so (C ABI declared in include/acehip.h).
+
+The library is built in-tree (``make -C ace-step-1.5_amd`` or
+``__graft_entry__.build()``) and loaded from this directory.  There is no
+fallback: if the shared object is missing or fails to load, every entry point
+raises — the product path never silently degrades to a CPU/eager path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_uint8, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libacehip.so")
+
+ACEHIP_F32 = 0
+ACEHIP_BF16 = 1
+
+# every symbol include/acehip.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "acehip_get_version", "acehip_last_error",
+    "acehip_dit_create", "acehip_dit_set_weight", "acehip_dit_finalize",
+    "acehip_dit_set_condition", "acehip_dit_forward", "acehip_dit_destroy",
+    "acehip_sampler_apg_euler", "acehip_sampler_axpy",
+    "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
+    "acehip_vae_encode", "acehip_vae_destroy",
+    "acehip_gemm_bf16", "acehip_attention_bf16",
+]
+
+
+class DiTCfg(ctypes.Structure):
+    _fields_ = [("hidden", c_int), ("intermediate", c_int), ("heads", c_int), ("kv_heads", c_int),
+                ("head_dim", c_int), ("layers", c_int), ("window", c_int), ("patch", c_int),
+                ("in_channels", c_int), ("out_channels", c_int), ("eps", c_float),
+                ("rope_theta", c_float), ("max_S", c_int), ("max_Bc", c_int), ("max_Lenc", c_int),
+                ("sliding", POINTER(c_uint8))]
+
+
+class VAECfg(ctypes.Structure):
+    _fields_ = [("encoder_hidden", c_int), ("decoder_channels", c_int), ("latent_channels", c_int),
+                ("audio_channels", c_int), ("n_blocks", c_int), ("ratios", c_int * 8),
+                ("multiples", c_int * 8), ("max_T", c_int), ("max_B", c_int),
+                ("with_encoder", c_int)]
+
+
+_LIB = None
+
+
+def _declare(lib):
+    P = c_void_p
+    sig = {
+        "acehip_get_version": (c_int, []),
+        "acehip_last_error": (c_char_p, []),
+        "acehip_dit_create": (c_int, [c_int, POINTER(DiTCfg), POINTER(c_void_p)]),
+        "acehip_dit_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
+        "acehip_dit_finalize": (c_int, [P]),
+        "acehip_dit_set_condition": (c_int, [P, P, c_int, c_int, P]),
+        "acehip_dit_forward": (c_int, [P, P, P, c_int, P, P, c_int, c_int, c_int, P, P]),
+        "acehip_dit_destroy": (c_int, [P]),
+        "acehip_sampler_apg_euler": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, c_int,
+                                             c_int, c_int, P]),
+        "acehip_sampler_axpy": (c_int, [P, P, c_int64, c_float, P]),
+        "acehip_vae_create": (c_int, [c_int, POINTER(VAECfg), POINTER(c_void_p)]),
+        "acehip_vae_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
+        "acehip_vae_finalize": (c_int, [P]),
+        "acehip_vae_decode": (c_int, [P, P, c_int, c_int, P, P]),
+        "acehip_vae_encode": (c_int, [P, P, c_int, c_int, P, P, P]),
+        "acehip_vae_destroy": (c_int, [P]),
+        "acehip_gemm_bf16": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
+        "acehip_attention_bf16": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                          c_float, P]),
+    }
+    for name, (res, args) in sig.items():
+        if not hasattr(lib, name):
+            continue  # reported by missing_exports()
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load libacehip.so (raises if it is missing — no fallback path exists)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"acehip: {LIB_PATH} not built; run `make -C ace-step-1.5_amd` "
+                               "or __graft_entry__.build()")
+        handle = ctypes.CDLL(LIB_PATH)
+        _declare(handle)
+        _LIB = handle
+    return _LIB
+
+
+def missing_exports():
+    l = lib()
+    return [n for n in EXPORTS if not hasattr(l, n)]
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().acehip_last_error()
+        raise RuntimeError(f"acehip {what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def stream_ptr(stream=None):
+    """HIP stream handle of a torch stream (current stream by default)."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return c_void_p(t.data_ptr()) if t is not None else None
+
+
+def shape_arg(shape):
+    return (c_int64 * len(shape))(*shape)

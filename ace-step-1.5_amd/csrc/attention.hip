@@ -1,0 +1,198 @@
+// attention.hip — flash attention forward for the DiT (head_dim 128, GQA).
+//
+// Covers all three attention flavours of the decoder (reference
+// AceStepAttention.forward base:289-371 via SDPA):
+//   * full bidirectional self-attention (odd layers),
+//   * bidirectional band |i−j| ≤ window (even "sliding" layers; only the
+//     KV tiles that intersect the band are visited — the reference's SDPA
+//     path computes the full S×S and masks it),
+//   * unmasked cross-attention over the cached encoder K/V (base:1384-1428:
+//     the decoder never masks encoder padding).
+//
+// Layout: q [B][H][Sq][128], k/v [B][KV][Sk][128] (head-major, written by
+// head_post), o token-major [B][Sq][o_ld] at column h·128.
+//
+// Structure: workgroup = 4 waves × 32 queries of one (b, head); KV tiles of
+// 64 keys staged in LDS (rows of 256 B, 16-B chunks XOR-swizzled so that the
+// K row reads (ds_read_b128) and the V transposed reads (ds_read_b64_tr_b16)
+// are bank-conflict free).  Per wave, v_mfma_f32_32x32x16_bf16 computes the
+// swapped score tile Sᵀ = K·Qᵀ, so each lane owns one query row: the row
+// max/sum is 32 in-register values plus one cross-half exchange.  Sᵀ's
+// accumulator registers, converted to bf16, are directly the B operand of
+// Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P).  Online softmax in the exp2 domain;
+// masked scores use a finite −1e30 sentinel (a row whose first tiles are
+// fully masked accumulates garbage that the first real tile's rescale zeroes).
+#include "kernels.h"
+
+namespace acehip {
+namespace {
+
+constexpr int QB = 128;    // queries per workgroup
+constexpr int KT = 64;     // keys per tile
+constexpr float NEG = -1e30f;
+
+__device__ __forceinline__ int kvoff(int row, int ch) {
+    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restrict__ q,
+                                                           const bf16_t *__restrict__ k,
+                                                           const bf16_t *__restrict__ v,
+                                                           bf16_t *__restrict__ o, int H, int KV,
+                                                           int Sq, int Sk, int window, float sl2,
+                                                           int64_t o_ld) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * KT * 256];
+    char *ldsK = lds, *ldsV = lds + KT * 256;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int b = blockIdx.z, hq = blockIdx.y, kvh = hq / (H / KV);
+    const int qblk = blockIdx.x * QB;
+    const int q0 = qblk + wave * 32;
+    const int qi = q0 + r;
+
+    // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[qi][16s + 8hh .. +8]
+    const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi, Sq - 1)) * 128;
+    bf16x8 qf[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8 *)(qp + 16 * s + 8 * hh);
+
+    const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    int kv_lo = 0, kv_hi = Sk;
+    if (window >= 0) {
+        kv_lo = max(0, qblk - window);
+        kv_hi = min(Sk, qblk + QB + window);
+    }
+    float m = NEG, l = 0.f;
+    f32x16 oacc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
+
+    for (int kv0 = (kv_lo / KT) * KT; kv0 < kv_hi; kv0 += KT) {
+        __syncthreads();
+        // stage K and V tiles: 64 rows × 16 chunks each; zero rows past Sk
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i;
+            const int row = c >> 4, ch = c & 15;
+            const int key = kv0 + row;
+            uint4 kk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+            if (key < Sk) {
+                kk = *(const uint4 *)(kp + (int64_t)key * 128 + ch * 8);
+                vv = *(const uint4 *)(vp + (int64_t)key * 128 + ch * 8);
+            }
+            *(uint4 *)(ldsK + kvoff(row, ch)) = kk;
+            *(uint4 *)(ldsV + kvoff(row, ch)) = vv;
+        }
+        __syncthreads();
+
+        // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
+        f32x16 st[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 kf = *(const bf16x8 *)(ldsK + kvoff(32 * t + r, 2 * s + hh));
+                st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
+            }
+        }
+        // scale (log2 domain) + mask + running max
+        float mx = NEG;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
+                bool ok = kj < Sk;
+                if (window >= 0) ok = ok && abs(qi - kj) <= window;
+                const float sv = ok ? st[t][j] * sl2 : NEG;
+                st[t][j] = sv;
+                mx = fmaxf(mx, sv);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m, mx);
+        const float alpha = exp2f(m - mn);
+        m = mn;
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float p = exp2f(st[t][j] - mn);
+                st[t][j] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+
+        // P (bf16) as the B operand: tile t, k-step s ← registers 8s..8s+7
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
+
+        // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads
+        const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int dc = 32 * dt + 16 * (g & 1);
+            const int chk = (dc >> 3) + (pp >> 1);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int kb = 32 * t + 16 * s + 4 * (g >> 1);
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) s16x4 *)(ldsV + kvoff(kb + qq, chk) + 8 * (pp & 1)));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) s16x4 *)(ldsV + kvoff(kb + 8 + qq, chk) + 8 * (pp & 1)));
+                    // whole-vector reinterpretation (per-element bit_cast<__bf16> insertion
+                    // is miscompiled by ROCm 7.2 hipcc: it keeps only the first dword)
+                    const s16x8 cat = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    const bf16x8 vf = __builtin_bit_cast(bf16x8, cat);
+                    oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
+                }
+        }
+    }
+
+    if (qi >= Sq) return;
+    const float inv = 1.0f / l;
+    bf16_t *op = o + ((int64_t)b * Sq + qi) * o_ld + hq * 128;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            const int d = 32 * dt + 8 * gg + 4 * hh;
+            float ov[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ov[j] = oacc[dt][4 * gg + j] * inv;
+            *(uint2 *)(op + d) = pack4(ov);
+        }
+}
+
+}  // namespace
+
+int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
+              int Sq, int Sk, int window, float scale, int64_t o_ld, hipStream_t s) {
+    if (B <= 0 || Sq <= 0) return 0;
+    if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
+    if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
+    dim3 grid((Sq + QB - 1) / QB, H, B);
+    attn_fwd_kernel<<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window,
+                                         scale * 1.4426950408889634f, o_ld);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // namespace acehip

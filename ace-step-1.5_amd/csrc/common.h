@@ -1,0 +1,94 @@
+// common.h — shared device/host helpers for libacehip (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+typedef uint16_t bf16_t;  // raw bf16 bits in memory
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+// ------------------------------------------------------------- bf16 math ---
+__host__ __device__ __forceinline__ float bf2f(bf16_t v) {
+    union { uint32_t u; float f; } x;
+    x.u = ((uint32_t)v) << 16;
+    return x.f;
+}
+// round-to-nearest-even; NaN preserved (quiet)
+__host__ __device__ __forceinline__ bf16_t f2bf(float f) {
+    union { uint32_t u; float f; } x;
+    x.f = f;
+    if ((x.u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((x.u >> 16) | 0x40);
+    uint32_t r = x.u + 0x7fffu + ((x.u >> 16) & 1u);
+    return (bf16_t)(r >> 16);
+}
+// round an fp32 value through bf16 (models one torch bf16 op's output rounding)
+__host__ __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+// pack/unpack 8 bf16 in a uint4
+__device__ __forceinline__ void unpack8(const uint4 &u, float *f) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = bf2f((bf16_t)(w[i] & 0xffff));
+        f[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16));
+    }
+}
+__device__ __forceinline__ uint4 pack8(const float *f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint2 pack4(const float *f) {
+    return make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                      (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+}
+__device__ __forceinline__ void unpack4(const uint2 &u, float *f) {
+    f[0] = bf2f((bf16_t)(u.x & 0xffff)); f[1] = bf2f((bf16_t)(u.x >> 16));
+    f[2] = bf2f((bf16_t)(u.y & 0xffff)); f[3] = bf2f((bf16_t)(u.y >> 16));
+}
+
+// ------------------------------------------------------- wave reductions ---
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// --------------------------------------------------------- LDS-DMA (glds) --
+// 16 bytes per lane, global → LDS; the LDS destination is lds_base + lane*16
+// (wave-uniform base).  gfx950 global_load_lds_dwordx4.
+__device__ __forceinline__ void glds16(const void *gsrc, void *lds_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)gsrc,
+                                     (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
+
+// bijective XCD-aware block remap (cdna_hip_programming.md §5 template)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// ------------------------------------------------------------ host side ---
+namespace acehip {
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+}  // namespace acehip
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return acehip::fail(-3, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+    } while (0)

@@ -1,0 +1,40 @@
+// conv.h — implicit-GEMM convolution arguments (see conv.hip).
+#pragma once
+#include "common.h"
+
+namespace acehip {
+
+// out[m·c_stride + c_off + phase][n] = Σ_{tap,ci} in[m·a_stride + tap·dil + a_off][ci] · W_phase[n][tap·Cin + ci] (+bias[n]) (+res)
+// epilogue writes the raw value to `out` and/or Snake(raw) (params sa = e^α,
+// sib = 1/(e^β+1e-9)) to `out_s` — the activation the NEXT convolution consumes.
+struct ConvArgs {
+    const bf16_t *in; int64_t L_in; int Cin;     // NLC input [L_in][Cin]
+    const bf16_t *W; int64_t w_pstride;          // packed [phases][N][taps·Cin]
+    const bf16_t *bias;                          // [N] or null
+    bf16_t *out;                                 // raw output [L_out][N] or null
+    bf16_t *out_s; const float *sa, *sib;        // snaked output or null
+    const bf16_t *res;                           // residual [L_out][N] or null (may alias out)
+    int64_t L_out; int N;
+    int64_t M;                                   // GEMM rows per phase
+    int taps, dil, a_stride, a_off, c_stride, c_off;
+};
+int conv_gemm(const ConvArgs &a, int phases, hipStream_t s);
+// final decoder conv: snaked NLC [L][Cin] → fp32 channels-first [Cout=2][L], k 7, no bias
+int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s);
+// encoder first conv: channels-first [Cin≤2][N] → raw + snaked NLC [N][Cout], k 7, bias
+int conv_in(const bf16_t *in, int64_t N, int Cin, const float *w, const float *bias, int Cout,
+            bf16_t *out, bf16_t *out_s, const float *sa, const float *sib, hipStream_t s);
+int cf_to_nlc(const bf16_t *in, int C, int64_t L, bf16_t *out, hipStream_t s);
+int gauss_sample(const bf16_t *h, int64_t T, int C, const bf16_t *eps, bf16_t *z, hipStream_t s);
+// weight-norm fusion + implicit-GEMM packing: w = g·v/‖v‖ (norm over all dims but 0)
+//   conv  v [Cout][Cin][k]  → Wp[co][tap·Cin+ci]
+//   convT v [Cin][Cout][2s] → Wp[r][co][tap·Cin+ci], tap0 = kernel r+s (input m−1), tap1 = kernel r
+int pack_conv_weight(const bf16_t *v, const bf16_t *g, int d0, int d1, int k, int transposed,
+                     int stride, bf16_t *Wp, hipStream_t s);
+// same fusion into fp32 [Cout][k][Cin] (for conv_out) or [Cout][Cin][k] (conv_in) layouts
+int fuse_conv_weight_f32(const bf16_t *v, const bf16_t *g, int d0, int d1, int k, int k_major,
+                         float *w, hipStream_t s);
+int snake_params(const bf16_t *alpha, const bf16_t *beta, int C, float *sa, float *sib, hipStream_t s);
+int cast_bf16_f32(const bf16_t *src, float *dst, int64_t n, hipStream_t s);
+
+}  // namespace acehip

@@ -1,0 +1,418 @@
+// conv.hip — Oobleck VAE convolutions as implicit GEMMs on MFMA.
+//
+// Activations are channels-last [L][C] bf16 (NLC), so every convolution of
+// the Oobleck decoder/encoder (reference spec acestep/models/mlx/
+// vae_model.py:24-230; diffusers AutoencoderOobleck) is one GEMM
+//   out[m·c_stride + c_off + phase][n] = Σ_tap Σ_ci in[m·a_stride + tap·dil + a_off][ci]·W[n][tap·Cin+ci]
+// with zero padding outside [0, L_in):
+//   * Conv1d k=7 dilation d (residual units):  taps 7, a_off −3d
+//   * Conv1d k=1:                              taps 1
+//   * ConvTranspose1d k=2s stride s pad s/2:   s phases r (gridDim.y); output rows
+//     m·s + r − s/2, each the GEMM of the 2 overlapping input rows [m−1 | m]
+//   * strided Conv1d k=2s (encoder):           taps 2s, a_stride s, a_off −s/2
+// Snake1d (x + 1/(e^β+1e-9)·sin(e^α·x)², vae_model.py:38-55) is applied ONCE,
+// in the epilogue of the conv that produces its input ("out_s"), instead of
+// in every consumer tile (a k=7 conv would recompute it 7× per N-tile); the
+// bias and the residual skip (OobleckResidualUnit, vae_model.py:77-87) are
+// fused in the same epilogue.  The residual may alias the raw output (each
+// element is read and written by the same lane).
+//
+// Tile 128×128×64, 4 waves (2×2) of v_mfma_f32_16x16x32_bf16; both operands
+// are staged one tile ahead — W by global_load_lds into a double buffer, the
+// A (im2col) tile through registers (its global loads are in flight during
+// the MFMAs of the current tile), XOR-swizzled for conflict-free ds_read_b128.
+#include "kernels.h"
+#include "conv.h"
+
+namespace acehip {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE = BM * BK * 2;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+template <bool RES, bool RAW, bool SN>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[4 * TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tilesN = a.N / BN;
+    const int64_t tilesM = (a.M + BM - 1) / BM;
+    const int64_t wg = xcd_remap(blockIdx.x, (int)(tilesM * tilesN));
+    const int64_t tm = wg / tilesN;
+    const int tn = (int)(wg % tilesN);     // N-fastest: neighbouring blocks share the A panel
+    const int64_t m0 = tm * BM;
+    const int n0 = tn * BN;
+    const int phase = blockIdx.y;
+    const bf16_t *Wp = a.W + (int64_t)phase * a.w_pstride;
+    const int K = a.taps * a.Cin;
+
+    const bf16_t *wsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        wsrc[i] = Wp + (int64_t)(n0 + r) * K + c * 8;
+    }
+    uint4 areg[4];
+    auto load_a = [&](int k0) {
+        const int tap = k0 / a.Cin, ci0 = k0 % a.Cin;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i;
+            const int row = c >> 3, ch = c & 7;
+            const int64_t m = m0 + row;
+            const int64_t pos = m * a.a_stride + (int64_t)tap * a.dil + a.a_off;
+            areg[i] = make_uint4(0, 0, 0, 0);
+            if (m < a.M && pos >= 0 && pos < a.L_in)
+                areg[i] = *(const uint4 *)(a.in + pos * a.Cin + ci0 + ch * 8);
+        }
+    };
+    auto store_a = [&](int buf) {
+        char *bx = lds + buf * 2 * TILE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i;
+            *(uint4 *)(bx + swz(c >> 3, c & 7)) = areg[i];
+        }
+    };
+    auto stage_w = [&](int buf, int k0) {
+        char *bw = lds + buf * 2 * TILE + TILE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16(wsrc[i] + k0, bw + (wave * 4 + i) * 1024);
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage_w(0, 0);
+    load_a(0);
+    store_a(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int fr = lane & 15, fc = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            stage_w(cur ^ 1, (kt + 1) * BK);
+            load_a((kt + 1) * BK);
+        }
+        const char *bx = lds + cur * 2 * TILE;
+        const char *bw = bx + TILE;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 xf[4], wf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xf[i] = *(const bf16x8 *)(bx + swz(wm * 64 + i * 16 + fr, ks * 4 + fc));
+                wf[i] = *(const bf16x8 *)(bw + swz(wn * 64 + i * 16 + fr, ks * 4 + fc));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        }
+        if (more) store_a(cur ^ 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + wm * 64 + i * 16 + fr;
+        const int64_t row = m * a.c_stride + a.c_off + phase;
+        if (m >= a.M || row < 0 || row >= a.L_out) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + fc * 4;
+            float bb[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
+            if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = rbf(acc[i][j][r] + bb[r]);   // conv output (bf16)
+            if constexpr (RES) {
+                float rr[4];
+                unpack4(*(const uint2 *)(a.res + row * a.N + n), rr);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = rbf(rr[r] + o[r]);
+            }
+            if constexpr (RAW) *(uint2 *)(a.out + row * a.N + n) = pack4(o);
+            if constexpr (SN) {
+                const float4 sa = *(const float4 *)(a.sa + n);
+                const float4 sb = *(const float4 *)(a.sib + n);
+                const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
+                float sn[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float s = sinf(av[r] * o[r]);
+                    sn[r] = o[r] + bv[r] * s * s;
+                }
+                *(uint2 *)(a.out_s + row * a.N + n) = pack4(sn);
+            }
+        }
+    }
+}
+
+// Final decoder conv (Cout = 2 audio channels, k=7, pad 3, no bias) on the
+// already-snaked input; fp32 channels-first output [2][L].  One block = 256
+// output positions; the 262-row halo window is staged channel-major in LDS so
+// consecutive lanes read consecutive positions.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_out_kernel(const bf16_t *__restrict__ in, int64_t L, int Cin,
+                                                       const float *__restrict__ w,  // [COUT][7][Cin]
+                                                       float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int P = 256 + 6;
+    bf16_t *xs = (bf16_t *)smem;   // [Cin][P]
+    float *ws = (float *)(smem + ((size_t)Cin * P * 2 + 15) / 16 * 16);
+    const int64_t t0 = (int64_t)blockIdx.x * 256;
+    for (int i = threadIdx.x; i < COUT * 7 * Cin; i += 256) ws[i] = w[i];
+    const int chunks = Cin / 8;
+    for (int c = threadIdx.x; c < P * chunks; c += 256) {
+        const int p = c / chunks, ch = c % chunks;
+        const int64_t pos = t0 - 3 + p;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (pos >= 0 && pos < L) v = *(const uint4 *)(in + pos * Cin + ch * 8);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xs[(ch * 8 + 2 * j) * P + p] = (bf16_t)(wv[j] & 0xffff);
+            xs[(ch * 8 + 2 * j + 1) * P + p] = (bf16_t)(wv[j] >> 16);
+        }
+    }
+    __syncthreads();
+    const int64_t t = t0 + threadIdx.x;
+    if (t >= L) return;
+    float acc[COUT];
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
+    for (int c = 0; c < Cin; ++c) {
+        const bf16_t *xr = xs + c * P + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const float x = bf2f(xr[k]);
+#pragma unroll
+            for (int o = 0; o < COUT; ++o) acc[o] += x * ws[(o * 7 + k) * Cin + c];
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) out[(int64_t)o * L + t] = acc[o];
+}
+
+// Encoder first conv: channels-first audio [Cin≤2][N] → NLC [N][Cout] raw + snaked, k=7 pad 3, bias.
+__global__ __launch_bounds__(256) void conv_in_kernel(const bf16_t *__restrict__ in, int64_t N, int Cin,
+                                                      const float *__restrict__ w,  // [Cout][Cin][7]
+                                                      const float *__restrict__ bias, int Cout,
+                                                      bf16_t *__restrict__ out, bf16_t *__restrict__ out_s,
+                                                      const float *__restrict__ sa,
+                                                      const float *__restrict__ sib) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= N) return;
+    float x[2][7];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const int64_t p = t - 3 + k;
+            x[c][k] = (c < Cin && p >= 0 && p < N) ? bf2f(in[(int64_t)c * N + p]) : 0.f;
+        }
+    for (int o = lane; o < Cout; o += 64) {
+        float acc = bias ? bias[o] : 0.f;
+        for (int c = 0; c < Cin; ++c)
+#pragma unroll
+            for (int k = 0; k < 7; ++k) acc += x[c][k] * w[(o * Cin + c) * 7 + k];
+        const float v = rbf(acc);
+        if (out) out[t * Cout + o] = f2bf(v);
+        if (out_s) {
+            const float s = sinf(sa[o] * v);
+            out_s[t * Cout + o] = f2bf(v + sib[o] * s * s);
+        }
+    }
+}
+
+__global__ void cf_to_nlc_kernel(const bf16_t *in, int C, int64_t L, bf16_t *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)C * L) return;
+    const int64_t t = i / C;
+    const int c = (int)(i % C);
+    out[i] = in[(int64_t)c * L + t];
+}
+
+// latent_dist.sample() (vae_model.py:285-304): h [T][2C] = (mean | scale) →
+// z [C][T] = mean + (softplus(scale) + 1e-4)·eps; eps == null → the mean
+__global__ void gauss_sample_kernel(const bf16_t *h, int64_t T, int C, const bf16_t *eps, bf16_t *z) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)C * T) return;
+    const int c = (int)(i / T);
+    const int64_t t = i % T;
+    const float mean = bf2f(h[t * 2 * C + c]);
+    float v = mean;
+    if (eps) {
+        const float sc = bf2f(h[t * 2 * C + C + c]);
+        const float sp = sc > 20.f ? sc : log1pf(expf(sc));
+        v = mean + rbf(rbf(sp) + 1e-4f) * bf2f(eps[i]);
+    }
+    z[i] = f2bf(v);
+}
+
+// weight-norm fusion: one block per dim-0 row of v (numel_row = d1·k)
+__global__ void pack_conv_weight_kernel(const bf16_t *v, const bf16_t *g, int d0, int d1, int k,
+                                        int transposed, int stride, bf16_t *Wp) {
+    const int i = blockIdx.x;                       // dim-0 index
+    const int nr = d1 * k;
+    const bf16_t *vr = v + (int64_t)i * nr;
+    __shared__ float red[256];
+    float ss = 0.f;
+    for (int e = threadIdx.x; e < nr; e += 256) {
+        const float x = bf2f(vr[e]);
+        ss += x * x;
+    }
+    red[threadIdx.x] = ss;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    const float scale = g ? bf2f(g[i]) / sqrtf(red[0]) : 1.0f;
+    for (int e = threadIdx.x; e < nr; e += 256) {
+        const int j = e / k, kk = e % k;
+        const float w = bf2f(vr[e]) * scale;
+        if (!transposed) {
+            // v [Cout=d0][Cin=d1][k] → Wp[co][tap·Cin + ci]
+            Wp[(int64_t)i * nr + (int64_t)kk * d1 + j] = f2bf(w);
+        } else {
+            // v [Cin=d0][Cout=d1][2s] → phase r = kk % s, tap = (kk < s) ? 1 : 0
+            const int s = stride, r = kk % s, tap = kk < s ? 1 : 0;
+            const int64_t K = 2 * (int64_t)d0;
+            Wp[((int64_t)r * d1 + j) * K + (int64_t)tap * d0 + i] = f2bf(w);
+        }
+    }
+}
+
+__global__ void fuse_conv_f32_kernel(const bf16_t *v, const bf16_t *g, int d0, int d1, int k, int k_major,
+                                     float *w) {
+    const int i = blockIdx.x;
+    const int nr = d1 * k;
+    const bf16_t *vr = v + (int64_t)i * nr;
+    __shared__ float red[256];
+    float ss = 0.f;
+    for (int e = threadIdx.x; e < nr; e += 256) {
+        const float x = bf2f(vr[e]);
+        ss += x * x;
+    }
+    red[threadIdx.x] = ss;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    const float scale = g ? bf2f(g[i]) / sqrtf(red[0]) : 1.0f;
+    for (int e = threadIdx.x; e < nr; e += 256) {
+        const int j = e / k, kk = e % k;
+        const float x = bf2f(vr[e]) * scale;
+        if (k_major) w[((int64_t)i * k + kk) * d1 + j] = x;   // [Cout][k][Cin]
+        else w[(int64_t)i * nr + e] = x;                       // [Cout][Cin][k]
+    }
+}
+
+__global__ void snake_params_kernel(const bf16_t *alpha, const bf16_t *beta, int C, float *sa, float *sib) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    sa[c] = expf(bf2f(alpha[c]));
+    sib[c] = 1.0f / (expf(bf2f(beta[c])) + 1e-9f);
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t *s, float *d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) d[i] = bf2f(s[i]);
+}
+
+}  // namespace
+
+int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
+    if (a.M <= 0) return 0;
+    if (a.N % BN || a.Cin % BK)
+        return fail(-1, "conv_gemm: N%128 and Cin%64 required (N=" + std::to_string(a.N) +
+                            " Cin=" + std::to_string(a.Cin) + ")");
+    if (!a.out && !a.out_s) return fail(-1, "conv_gemm: no output");
+    if (a.out_s && (!a.sa || !a.sib)) return fail(-1, "conv_gemm: snake params");
+    const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
+    if (tiles >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
+    dim3 grid((unsigned)tiles, phases);
+    const bool rs = a.res != nullptr, raw = a.out != nullptr, sn = a.out_s != nullptr;
+#define L(R, W, S) conv_gemm_kernel<R, W, S><<<grid, 256, 0, s>>>(a)
+    if (rs) {
+        if (raw && sn) L(true, true, true); else if (raw) L(true, true, false); else L(true, false, true);
+    } else {
+        if (raw && sn) L(false, true, true); else if (raw) L(false, true, false); else L(false, false, true);
+    }
+#undef L
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s) {
+    if (Cout != 2 || Cin % 8) return fail(-1, "conv_out: Cout must be 2, Cin%8 == 0");
+    const size_t smem = ((size_t)Cin * 262 * 2 + 15) / 16 * 16 + (size_t)2 * 7 * Cin * 4;
+    conv_out_kernel<2><<<(unsigned)((L + 255) / 256), 256, smem, s>>>(in_s, L, Cin, w, out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int conv_in(const bf16_t *in, int64_t N, int Cin, const float *w, const float *bias, int Cout, bf16_t *out,
+            bf16_t *out_s, const float *sa, const float *sib, hipStream_t s) {
+    if (Cin > 2) return fail(-1, "conv_in: at most 2 input channels");
+    conv_in_kernel<<<(unsigned)((N + 3) / 4), 256, 0, s>>>(in, N, Cin, w, bias, Cout, out, out_s, sa, sib);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int cf_to_nlc(const bf16_t *in, int C, int64_t L, bf16_t *out, hipStream_t s) {
+    const int64_t n = (int64_t)C * L;
+    cf_to_nlc_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, C, L, out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int gauss_sample(const bf16_t *h, int64_t T, int C, const bf16_t *eps, bf16_t *z, hipStream_t s) {
+    const int64_t n = (int64_t)C * T;
+    gauss_sample_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(h, T, C, eps, z);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pack_conv_weight(const bf16_t *v, const bf16_t *g, int d0, int d1, int k, int transposed, int stride,
+                     bf16_t *Wp, hipStream_t s) {
+    if (transposed && k != 2 * stride) return fail(-1, "pack_conv_weight: convT kernel must be 2*stride");
+    pack_conv_weight_kernel<<<d0, 256, 0, s>>>(v, g, d0, d1, k, transposed, stride, Wp);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int fuse_conv_weight_f32(const bf16_t *v, const bf16_t *g, int d0, int d1, int k, int k_major, float *w,
+                         hipStream_t s) {
+    fuse_conv_f32_kernel<<<d0, 256, 0, s>>>(v, g, d0, d1, k, k_major, w);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int snake_params(const bf16_t *alpha, const bf16_t *beta, int C, float *sa, float *sib, hipStream_t s) {
+    snake_params_kernel<<<(C + 255) / 256, 256, 0, s>>>(alpha, beta, C, sa, sib);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int cast_bf16_f32(const bf16_t *src, float *dst, int64_t n, hipStream_t s) {
+    cast_bf16_f32_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // namespace acehip

@@ -1,0 +1,541 @@
+// dit.hip — the DiT runtime behind acehip_dit_* (C ABI in include/acehip.h).
+//
+// Owns the packed bf16 weights, the cross-attention K/V cache and a
+// workspace sized at create time; acehip_dit_forward enqueues one whole
+// AceStepDiTModel.forward (reference base:1303-1507) on the caller's stream
+// with no allocation and no host synchronisation.
+//
+// Weight packing (from the reference state-dict names):
+//   self q|k|v rows concatenated → one QKV GEMM (N = q + 2kv)
+//   cross k|v rows concatenated → one GEMM per layer at set_condition
+//   gate/up interleaved in 32-row panels → one GEMM with a SwiGLU epilogue
+//   proj_in  Conv1d [D][192][2]  → [D][2·192] (k-major) so the patch GEMM
+//            reads [T][192] rows pairwise with no im2col copy
+//   proj_out ConvT  [D][64][2]   → [2·64][D] so the GEMM output [S][128] is
+//            the de-patchified [2S][64] sequence in place
+//   scale_shift_tables of all layers contiguous → one modulation launch
+#include <map>
+#include <cmath>
+#include <vector>
+#include <cstring>
+
+#include "kernels.h"
+#include "../../include/acehip.h"
+
+using namespace acehip;
+
+namespace {
+
+enum PackKind { P_COPY, P_GU_GATE, P_GU_UP, P_PROJ_IN, P_PROJ_OUT_W, P_PROJ_OUT_B, P_F32 };
+
+struct Slot {
+    bf16_t *dst = nullptr;
+    std::vector<int64_t> shape;
+    PackKind kind = P_COPY;
+    bool set = false;
+    float *dst_f32 = nullptr;
+};
+
+}  // namespace
+
+struct acehip_dit {
+    int device = 0;
+    acehip_dit_cfg cfg{};
+    std::vector<uint8_t> sliding;
+    int D = 0, F = 0, qd = 0, kvd = 0, L = 0;
+    bool finalized = false, have_cond = false;
+    int cond_Bc = 0, cond_Lenc = 0;
+
+    std::vector<void *> allocs;
+    std::map<std::string, Slot> slots;
+
+    // weights
+    bf16_t *tables = nullptr;   // [L][6][D]
+    struct Layer {
+        bf16_t *n_sa, *n_ca, *n_mlp, *wqkv, *wo, *qn, *kn, *cqn, *ckn, *wcq, *wckv, *wco, *wgu, *wdown;
+    };
+    std::vector<Layer> layers;
+    bf16_t *sst_out, *win, *bin, *wce, *bce, *norm_out, *wout, *bout;
+    bf16_t *te_l1[2], *te_b1[2], *te_l2[2], *te_b2[2], *te_tp[2], *te_btp[2];
+    float *freqs = nullptr;          // [128] sinusoid frequencies
+    float *inv_freq_host = nullptr;  // optional override, [hd/2]
+    std::vector<float> inv_freq_override;
+    bf16_t *rope_cos = nullptr, *rope_sin = nullptr;   // [max_S][hd]
+
+    // workspace
+    bf16_t *X, *XN, *QKV, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
+    bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
+    bf16_t *Kc, *Vc, *E, *KVtmp;
+    bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
+    size_t tmp_elems = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+bf16_t *dalloc(acehip_dit *h, size_t elems) {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(elems, 1) * 2) != hipSuccess) return nullptr;
+    h->allocs.push_back(p);
+    return (bf16_t *)p;
+}
+
+void add_slot(acehip_dit *h, const std::string &name, bf16_t *dst, std::vector<int64_t> shape,
+              PackKind kind = P_COPY) {
+    Slot s;
+    s.dst = dst;
+    s.shape = std::move(shape);
+    s.kind = kind;
+    h->slots[name] = s;
+}
+
+int64_t numel(const std::vector<int64_t> &s) {
+    int64_t n = 1;
+    for (auto v : s) n *= v;
+    return n;
+}
+
+// host-side bf16 rounding (same as device f2bf)
+inline bf16_t hf2bf(float f) { return f2bf(f); }
+
+int build_rope(acehip_dit *h) {
+    const int hd = h->cfg.head_dim, S = h->cfg.max_S;
+    std::vector<float> inv(hd / 2);
+    for (int i = 0; i < hd / 2; ++i) {
+        float v;
+        if (!h->inv_freq_override.empty()) v = h->inv_freq_override[i];
+        else v = 1.0f / powf(h->cfg.rope_theta, (float)(2 * i) / (float)hd);
+        inv[i] = bf2f(hf2bf(v));   // model.to(bf16) casts the inv_freq buffer (init_service_loader.py:81-89)
+    }
+    std::vector<bf16_t> c((size_t)S * hd), s((size_t)S * hd);
+    for (int p = 0; p < S; ++p)
+        for (int i = 0; i < hd; ++i) {
+            const float f = (float)p * inv[i % (hd / 2)];
+            c[(size_t)p * hd + i] = hf2bf((float)cos((double)f));
+            s[(size_t)p * hd + i] = hf2bf((float)sin((double)f));
+        }
+    HIP_TRY(hipMemcpy(h->rope_cos, c.data(), c.size() * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->rope_sin, s.data(), s.size() * 2, hipMemcpyHostToDevice));
+    return 0;
+}
+
+}  // namespace
+
+namespace acehip {
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace acehip
+
+extern "C" {
+
+int acehip_get_version(void) { return ACEHIP_VERSION; }
+const char *acehip_last_error(void) { return g_err.c_str(); }
+
+int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
+    if (!cfg || !out) return fail(ACEHIP_E_ARG, "dit_create: null argument");
+    if (cfg->head_dim != 128) return fail(ACEHIP_E_ARG, "dit_create: head_dim must be 128");
+    if (cfg->hidden % 256 || cfg->intermediate % 64 || cfg->heads % cfg->kv_heads)
+        return fail(ACEHIP_E_ARG, "dit_create: unsupported dims");
+    if (cfg->patch != 2 || cfg->in_channels != 192 || cfg->out_channels != 64)
+        return fail(ACEHIP_E_ARG, "dit_create: patch 2 / 192 in / 64 out required");
+    if (cfg->max_Bc > 16 || cfg->max_Bc <= 0 || cfg->max_S <= 0 || cfg->max_Lenc <= 0)
+        return fail(ACEHIP_E_ARG, "dit_create: max_Bc in [1,16], max_S/max_Lenc > 0");
+    HIP_TRY(hipSetDevice(device));
+    auto *h = new acehip_dit();
+    h->device = device;
+    h->cfg = *cfg;
+    h->D = cfg->hidden; h->F = cfg->intermediate; h->L = cfg->layers;
+    h->qd = cfg->heads * cfg->head_dim; h->kvd = cfg->kv_heads * cfg->head_dim;
+    h->sliding.resize(h->L);
+    for (int i = 0; i < h->L; ++i) h->sliding[i] = cfg->sliding ? cfg->sliding[i] : ((i + 1) % 2);
+    h->cfg.sliding = nullptr;
+    const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L;
+    bool ok = true;
+    auto A = [&](size_t n) { bf16_t *p = dalloc(h, n); ok = ok && p; return p; };
+
+    h->tables = A((size_t)L * 6 * D);
+    h->layers.resize(L);
+    for (int i = 0; i < L; ++i) {
+        auto &ly = h->layers[i];
+        ly.n_sa = A(D); ly.n_ca = A(D); ly.n_mlp = A(D);
+        ly.wqkv = A((size_t)(qd + 2 * kvd) * D); ly.wo = A((size_t)D * qd);
+        ly.qn = A(128); ly.kn = A(128); ly.cqn = A(128); ly.ckn = A(128);
+        ly.wcq = A((size_t)qd * D); ly.wckv = A((size_t)2 * kvd * D); ly.wco = A((size_t)D * qd);
+        ly.wgu = A((size_t)2 * F * D); ly.wdown = A((size_t)D * F);
+        if (!ok) break;
+        const std::string p = "layers." + std::to_string(i);
+        add_slot(h, p + ".scale_shift_table", h->tables + (size_t)i * 6 * D, {1, 6, D});
+        add_slot(h, p + ".self_attn_norm.weight", ly.n_sa, {D});
+        add_slot(h, p + ".cross_attn_norm.weight", ly.n_ca, {D});
+        add_slot(h, p + ".mlp_norm.weight", ly.n_mlp, {D});
+        add_slot(h, p + ".self_attn.q_proj.weight", ly.wqkv, {qd, D});
+        add_slot(h, p + ".self_attn.k_proj.weight", ly.wqkv + (size_t)qd * D, {kvd, D});
+        add_slot(h, p + ".self_attn.v_proj.weight", ly.wqkv + (size_t)(qd + kvd) * D, {kvd, D});
+        add_slot(h, p + ".self_attn.o_proj.weight", ly.wo, {D, qd});
+        add_slot(h, p + ".self_attn.q_norm.weight", ly.qn, {128});
+        add_slot(h, p + ".self_attn.k_norm.weight", ly.kn, {128});
+        add_slot(h, p + ".cross_attn.q_proj.weight", ly.wcq, {qd, D});
+        add_slot(h, p + ".cross_attn.k_proj.weight", ly.wckv, {kvd, D});
+        add_slot(h, p + ".cross_attn.v_proj.weight", ly.wckv + (size_t)kvd * D, {kvd, D});
+        add_slot(h, p + ".cross_attn.o_proj.weight", ly.wco, {D, qd});
+        add_slot(h, p + ".cross_attn.q_norm.weight", ly.cqn, {128});
+        add_slot(h, p + ".cross_attn.k_norm.weight", ly.ckn, {128});
+        add_slot(h, p + ".mlp.gate_proj.weight", ly.wgu, {F, D}, P_GU_GATE);
+        add_slot(h, p + ".mlp.up_proj.weight", ly.wgu, {F, D}, P_GU_UP);
+        add_slot(h, p + ".mlp.down_proj.weight", ly.wdown, {D, F});
+    }
+    h->sst_out = A(2 * D); h->win = A((size_t)D * 384); h->bin = A(D);
+    h->wce = A((size_t)D * D); h->bce = A(D); h->norm_out = A(D);
+    h->wout = A((size_t)128 * D); h->bout = A(128);
+    const char *te_names[2] = {"time_embed", "time_embed_r"};
+    for (int e = 0; e < 2; ++e) {
+        h->te_l1[e] = A((size_t)D * 256); h->te_b1[e] = A(D);
+        h->te_l2[e] = A((size_t)D * D); h->te_b2[e] = A(D);
+        h->te_tp[e] = A((size_t)6 * D * D); h->te_btp[e] = A(6 * D);
+        if (!ok) break;
+        const std::string p = te_names[e];
+        add_slot(h, p + ".linear_1.weight", h->te_l1[e], {D, 256});
+        add_slot(h, p + ".linear_1.bias", h->te_b1[e], {D});
+        add_slot(h, p + ".linear_2.weight", h->te_l2[e], {D, D});
+        add_slot(h, p + ".linear_2.bias", h->te_b2[e], {D});
+        add_slot(h, p + ".time_proj.weight", h->te_tp[e], {6 * D, D});
+        add_slot(h, p + ".time_proj.bias", h->te_btp[e], {6 * D});
+    }
+    if (ok) {
+        add_slot(h, "scale_shift_table", h->sst_out, {1, 2, D});
+        add_slot(h, "proj_in.1.weight", h->win, {D, 192, 2}, P_PROJ_IN);
+        add_slot(h, "proj_in.1.bias", h->bin, {D});
+        add_slot(h, "condition_embedder.weight", h->wce, {D, D});
+        add_slot(h, "condition_embedder.bias", h->bce, {D});
+        add_slot(h, "norm_out.weight", h->norm_out, {D});
+        add_slot(h, "proj_out.1.weight", h->wout, {D, 64, 2}, P_PROJ_OUT_W);
+        add_slot(h, "proj_out.1.bias", h->bout, {64}, P_PROJ_OUT_B);
+    }
+    // workspace
+    const size_t S = cfg->max_S, Bc = cfg->max_Bc, M = S * Bc, Le = cfg->max_Lenc;
+    h->X = A(M * D); h->XN = A(M * D); h->QKV = A(M * (qd + 2 * kvd));
+    h->Qh = A(M * qd); h->Kh = A(M * kvd); h->Vh = A(M * kvd); h->AO = A(M * qd);
+    h->Hb = A(M * F); h->Xin = A(M * 384); h->O2 = A(M * 128);
+    for (int e = 0; e < 2; ++e) {
+        h->emb[e] = A(Bc * 256); h->temb_e[e] = A(Bc * D); h->proj_e[e] = A(Bc * 6 * D);
+    }
+    h->h1 = A(Bc * D); h->temb = A(Bc * D); h->proj = A(Bc * 6 * D);
+    h->mod = A((size_t)L * Bc * 6 * D); h->mod_out = A(Bc * 2 * D);
+    h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
+    h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd);
+    h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
+    h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
+    h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
+    void *fr = nullptr;
+    if (ok && hipMalloc(&fr, 128 * sizeof(float)) == hipSuccess) {
+        h->allocs.push_back(fr);
+        h->freqs = (float *)fr;
+        float f[128];
+        for (int i = 0; i < 128; ++i)   // torch: exp(-ln(1e4) * arange(128, f32) / 128) in fp32 (base:239-241)
+            f[i] = expf((-9.210340371976184f * (float)i) / 128.0f);
+        ok = hipMemcpy(h->freqs, f, sizeof(f), hipMemcpyHostToDevice) == hipSuccess;
+    } else {
+        ok = false;
+    }
+    if (!ok) {
+        acehip_dit_destroy(h);
+        return fail(ACEHIP_E_OOM, "dit_create: device allocation failed");
+    }
+    *out = h;
+    return 0;
+}
+
+int acehip_dit_set_weight(acehip_dit *h, const char *name, const void *ptr, int dtype, int ndim,
+                          const int64_t *shape, int on_device) {
+    if (!h || !name || !ptr || !shape) return fail(ACEHIP_E_ARG, "dit_set_weight: null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    std::string nm(name);
+    if (nm.rfind("decoder.", 0) == 0) nm = nm.substr(8);
+    if (nm == "_timestep_freqs" || nm == "_rope_inv_freq") {
+        // optional overrides computed by the caller's torch (exact reference constants), fp32
+        if (dtype != ACEHIP_F32) return fail(ACEHIP_E_ARG, nm + ": fp32 required");
+        const int n = (int)shape[0];
+        std::vector<float> v(n);
+        HIP_TRY(hipMemcpy(v.data(), ptr, n * 4, on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+        if (nm == "_timestep_freqs") {
+            if (n != 128) return fail(ACEHIP_E_ARG, "_timestep_freqs must have 128 entries");
+            HIP_TRY(hipMemcpy(h->freqs, v.data(), 512, hipMemcpyHostToDevice));
+        } else {
+            if (n != h->cfg.head_dim / 2) return fail(ACEHIP_E_ARG, "_rope_inv_freq size");
+            h->inv_freq_override = v;
+        }
+        return 0;
+    }
+    if (nm == "rotary_emb.inv_freq") return 0;  // non-persistent buffer; recomputed
+    auto it = h->slots.find(nm);
+    if (it == h->slots.end()) return fail(ACEHIP_E_NAME, "dit_set_weight: unknown weight " + nm);
+    Slot &s = it->second;
+    std::vector<int64_t> sh(shape, shape + ndim);
+    if (sh != s.shape) {
+        std::string e = "dit_set_weight: shape mismatch for " + nm + " got [";
+        for (auto v : sh) e += std::to_string(v) + ",";
+        e += "] want [";
+        for (auto v : s.shape) e += std::to_string(v) + ",";
+        return fail(ACEHIP_E_ARG, e + "]");
+    }
+    const int64_t n = numel(sh);
+    if (dtype != ACEHIP_F32 && dtype != ACEHIP_BF16) return fail(ACEHIP_E_ARG, "dtype");
+    // bring to a contiguous bf16 device source
+    const bf16_t *src = nullptr;
+    std::vector<bf16_t> hb;
+    if (s.kind == P_PROJ_IN || s.kind == P_PROJ_OUT_W || s.kind == P_PROJ_OUT_B) {
+        // small: repack on host
+        std::vector<float> f(n);
+        if (dtype == ACEHIP_F32) {
+            HIP_TRY(hipMemcpy(f.data(), ptr, n * 4, on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+        } else {
+            std::vector<bf16_t> b(n);
+            HIP_TRY(hipMemcpy(b.data(), ptr, n * 2, on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+            for (int64_t i = 0; i < n; ++i) f[i] = bf2f(b[i]);
+        }
+        hb.resize(s.kind == P_PROJ_OUT_B ? 128 : n);
+        if (s.kind == P_PROJ_IN) {         // [D][192][2] → [D][k*192 + c]
+            const int64_t D = sh[0];
+            for (int64_t o = 0; o < D; ++o)
+                for (int c = 0; c < 192; ++c)
+                    for (int k = 0; k < 2; ++k) hb[o * 384 + k * 192 + c] = hf2bf(f[(o * 192 + c) * 2 + k]);
+        } else if (s.kind == P_PROJ_OUT_W) {   // [D][64][2] → [k*64 + o][D]
+            const int64_t D = sh[0];
+            for (int64_t c = 0; c < D; ++c)
+                for (int o = 0; o < 64; ++o)
+                    for (int k = 0; k < 2; ++k) hb[(k * 64 + o) * D + c] = hf2bf(f[(c * 64 + o) * 2 + k]);
+        } else {                               // bias [64] → [k*64 + o]
+            for (int k = 0; k < 2; ++k)
+                for (int o = 0; o < 64; ++o) hb[k * 64 + o] = hf2bf(f[o]);
+        }
+        HIP_TRY(hipMemcpy(s.dst, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+        s.set = true;
+        return 0;
+    }
+    if (dtype == ACEHIP_F32) {
+        // cast through the staging buffer in chunks
+        // tmp holds tmp_elems floats (4·tmp_elems bytes)
+        const float *fsrc = (const float *)ptr;
+        float *fstage = (float *)h->tmp;
+        if (s.kind == P_COPY) {
+            // chunked cast straight into the destination
+            const int64_t chunk = (int64_t)h->tmp_elems;
+            for (int64_t off = 0; off < n; off += chunk) {
+                const int64_t c = std::min(chunk, n - off);
+                HIP_TRY(hipMemcpy(fstage, fsrc + off, c * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+                int rc = cast_f32_bf16(fstage, s.dst + off, c, 0);
+                if (rc) return rc;
+                HIP_TRY(hipDeviceSynchronize());
+            }
+            s.set = true;
+            return 0;
+        }
+        if ((size_t)n * 6 > h->tmp_elems * 4) return fail(ACEHIP_E_ARG, "fp32 weight too large for staging; pass bf16");
+        HIP_TRY(hipMemcpy(fstage, fsrc, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+        bf16_t *b16 = h->tmp + n * 2;   // bf16 copy right after the fp32 staging
+        int rc = cast_f32_bf16(fstage, b16, n, 0);
+        if (rc) return rc;
+        HIP_TRY(hipDeviceSynchronize());
+        src = b16;
+    } else {
+        if (s.kind == P_COPY) {
+            HIP_TRY(hipMemcpy(s.dst, ptr, n * 2, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+            s.set = true;
+            return 0;
+        }
+        src = (const bf16_t *)ptr;
+    }
+    const hipMemcpyKind kind = (dtype == ACEHIP_F32 || on_device) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (s.kind == P_GU_GATE || s.kind == P_GU_UP) {
+        const int64_t F = sh[0], K = sh[1];
+        bf16_t *dst = s.dst + (s.kind == P_GU_UP ? 32 * K : 0);
+        HIP_TRY(hipMemcpy2D(dst, 64 * K * 2, src, 32 * K * 2, 32 * K * 2, F / 32, kind));
+        s.set = true;
+        return 0;
+    }
+    return fail(ACEHIP_E_ARG, "dit_set_weight: unhandled pack kind");
+}
+
+int acehip_dit_finalize(acehip_dit *h) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    std::string missing;
+    for (auto &kv : h->slots)
+        if (!kv.second.set) missing += kv.first + " ";
+    if (!missing.empty()) return fail(ACEHIP_E_STATE, "dit_finalize: missing weights: " + missing.substr(0, 400));
+    if (h->F % 32) return fail(ACEHIP_E_ARG, "intermediate must be a multiple of 32");
+    int rc = build_rope(h);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    h->finalized = true;
+    return 0;
+}
+
+int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, void *stream) {
+    if (!h || !enc) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized) return fail(ACEHIP_E_STATE, "set_condition before finalize");
+    if (Bc <= 0 || Bc > h->cfg.max_Bc || Lenc <= 0 || Lenc > h->cfg.max_Lenc)
+        return fail(ACEHIP_E_ARG, "set_condition: Bc/Lenc out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int D = h->D, kvd = h->kvd, M = Bc * Lenc;
+    GemmArgs g{};
+    g.A = (const bf16_t *)enc; g.lda = D; g.W = h->wce; g.ldw = D; g.C = h->E; g.ldc = D;
+    g.M = M; g.N = D; g.K = D; g.epi = EPI_STORE; g.bias = h->bce;
+    int rc = gemm(g, s);
+    if (rc) return rc;
+    const size_t per = (size_t)Bc * kvd * Lenc;
+    for (int l = 0; l < h->L; ++l) {
+        GemmArgs k{};
+        k.A = h->E; k.lda = D; k.W = h->layers[l].wckv; k.ldw = D; k.C = h->KVtmp; k.ldc = 2 * kvd;
+        k.M = M; k.N = 2 * kvd; k.K = D; k.epi = EPI_STORE;
+        if ((rc = gemm(k, s))) return rc;
+        HeadPostArgs p{};
+        p.src = h->KVtmp; p.ld_src = 2 * kvd; p.B = Bc; p.S = Lenc;
+        p.nq = 0; p.nk = h->cfg.kv_heads; p.nv = h->cfg.kv_heads;
+        p.kw = h->layers[l].ckn; p.k = h->Kc + l * per; p.v = h->Vc + l * per;
+        p.S_dst = Lenc; p.eps = h->cfg.eps;
+        if ((rc = head_post(p, s))) return rc;
+    }
+    h->have_cond = true;
+    h->cond_Bc = Bc;
+    h->cond_Lenc = Lenc;
+    return 0;
+}
+
+int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, const float *t,
+                       const float *t_r, int t_stride, int Bc, int T, void *vt_out, void *stream) {
+    if (!h || !xt || !ctx || !t || !t_r || !vt_out) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized || !h->have_cond) return fail(ACEHIP_E_STATE, "forward before finalize/set_condition");
+    if (Bc != h->cond_Bc) return fail(ACEHIP_E_ARG, "forward: Bc differs from set_condition");
+    const int S = (T + 1) / 2;
+    if (T <= 0 || S > h->cfg.max_S || Bx <= 0 || Bc % Bx) return fail(ACEHIP_E_ARG, "forward: T/Bx out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L, M = Bc * S;
+    const int H = h->cfg.heads, KV = h->cfg.kv_heads, Le = h->cond_Lenc;
+    const float eps = h->cfg.eps, scale = 1.0f / sqrtf((float)h->cfg.head_dim);
+    int rc;
+#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
+    // timestep embeddings: temb = temb_t + temb_r, proj = proj_t + proj_r (base:1340-1344)
+    for (int e = 0; e < 2; ++e) {
+        RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
+        RUN(gemv_small(h->emb[e], 256, h->te_l1[e], h->te_b1[e], h->h1, D, Bc, D, 256, 0, s));
+        RUN(gemv_small(h->h1, D, h->te_l2[e], h->te_b2[e], h->temb_e[e], D, Bc, D, D, 1, s));
+        RUN(gemv_small(h->temb_e[e], D, h->te_tp[e], h->te_btp[e], h->proj_e[e], 6 * D, Bc, 6 * D, D, 1, s));
+    }
+    RUN(add_bf16(h->temb_e[0], h->temb_e[1], h->temb, (int64_t)Bc * D, s));
+    RUN(add_bf16(h->proj_e[0], h->proj_e[1], h->proj, (int64_t)Bc * 6 * D, s));
+    RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s));
+    RUN(modulation(h->sst_out, 1, 2, h->temb, Bc, D, h->mod_out, s));
+
+    // proj_in (base:1347-1358)
+    RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
+    GemmArgs g{};
+    g.A = h->Xin; g.lda = 384; g.W = h->win; g.ldw = 384; g.C = h->X; g.ldc = D;
+    g.M = M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
+    RUN(gemm(g, s));
+
+    const size_t cper = (size_t)Bc * kvd * Le;
+    for (int l = 0; l < L; ++l) {
+        const auto &ly = h->layers[l];
+        const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
+        const int64_t mbs = 6 * D;
+        // --- self-attention with AdaLN-Zero (base:499-511)
+        RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, M, D, eps, s));
+        GemmArgs q{};
+        q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D; q.C = h->QKV; q.ldc = qd + 2 * kvd;
+        q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_STORE;
+        RUN(gemm(q, s));
+        HeadPostArgs hp{};
+        hp.src = h->QKV; hp.ld_src = qd + 2 * kvd; hp.B = Bc; hp.S = S;
+        hp.nq = H; hp.nk = KV; hp.nv = KV; hp.qw = ly.qn; hp.kw = ly.kn;
+        hp.cos = h->rope_cos; hp.sin = h->rope_sin;
+        hp.q = h->Qh; hp.k = h->Kh; hp.v = h->Vh; hp.S_dst = S; hp.eps = eps;
+        RUN(head_post(hp, s));
+        RUN(attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S,
+                      h->sliding[l] ? h->cfg.window : -1, scale, qd, s));
+        GemmArgs o{};
+        o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
+        o.M = M; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
+        o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
+        RUN(gemm(o, s));
+        // --- cross-attention, plain residual (base:513-526)
+        RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
+        GemmArgs cq{};
+        cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D; cq.C = h->QKV; cq.ldc = qd;
+        cq.M = M; cq.N = qd; cq.K = D; cq.epi = EPI_STORE;
+        RUN(gemm(cq, s));
+        HeadPostArgs cp{};
+        cp.src = h->QKV; cp.ld_src = qd; cp.B = Bc; cp.S = S; cp.nq = H; cp.qw = ly.cqn;
+        cp.q = h->Qh; cp.S_dst = S; cp.eps = eps;
+        RUN(head_post(cp, s));
+        RUN(attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd, s));
+        GemmArgs co{};
+        co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
+        co.M = M; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
+        RUN(gemm(co, s));
+        // --- SwiGLU MLP with AdaLN-Zero (base:528-533)
+        RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s));
+        GemmArgs gu{};
+        gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
+        gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;
+        RUN(gemm(gu, s));
+        GemmArgs dn{};
+        dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
+        dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
+        dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
+        RUN(gemm(dn, s));
+    }
+    // norm_out AdaLN + proj_out (base:1491-1501)
+    RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s));
+    GemmArgs po{};
+    po.A = h->XN; po.lda = D; po.W = h->wout; po.ldw = D;
+    po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
+    po.M = M; po.N = 128; po.K = D; po.epi = EPI_STORE; po.bias = h->bout;
+    RUN(gemm(po, s));
+    if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
+#undef RUN
+    return 0;
+}
+
+int acehip_dit_destroy(acehip_dit *h) {
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    for (void *p : h->allocs) (void)hipFree(p);
+    delete h;
+    return 0;
+}
+
+int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float guidance,
+                             float dt, int apply_cfg, int first_step, int out_mode, void *stream) {
+    if (!vt || !xt || (apply_cfg > 0 && !ra)) return fail(ACEHIP_E_ARG, "null argument");
+    return apg_euler((const bf16_t *)vt, (bf16_t *)xt, (bf16_t *)ra, B, T, C, guidance, dt, apply_cfg,
+                     first_step, out_mode, (hipStream_t)stream);
+}
+
+int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream) {
+    if (!vt || !xt) return fail(ACEHIP_E_ARG, "null argument");
+    return axpy_bf16((const bf16_t *)vt, (bf16_t *)xt, n, s, (hipStream_t)stream);
+}
+
+int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,
+                     int K, const void *bias, void *stream) {
+    GemmArgs g{};
+    g.A = (const bf16_t *)A; g.lda = lda; g.W = (const bf16_t *)W; g.ldw = ldw;
+    g.C = (bf16_t *)C; g.ldc = ldc; g.M = M; g.N = N; g.K = K; g.epi = EPI_STORE;
+    g.bias = (const bf16_t *)bias;
+    return gemm(g, (hipStream_t)stream);
+}
+
+int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,
+                          int Sq, int Sk, int window, float scale, void *stream) {
+    return attention((const bf16_t *)q, (const bf16_t *)k, (const bf16_t *)v, (bf16_t *)o, B, H, KV, Sq,
+                     Sk, window, scale, (int64_t)H * 128, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// kernels.h — launchers for every device kernel of libacehip (internal C++ API).
+#pragma once
+#include "common.h"
+
+namespace acehip {
+
+// ------------------------------------------------------------------ GEMM ---
+enum GemmEpi {
+    EPI_STORE = 0,       // C = bf16(acc + bias)
+    EPI_GATED_RES = 1,   // C = bf16(res + bf16(bf16(acc) * gate[b][n]))   (AdaLN-Zero gated residual)
+    EPI_RES = 2,         // C = bf16(res + bf16(acc))                       (plain residual)
+    EPI_SWIGLU = 3,      // packed [gate|up] blocks of 32 rows → C[M, N/2] = bf16(silu(g)·u)
+};
+
+struct GemmArgs {
+    const bf16_t *A; int64_t lda;   // [M, K]
+    const bf16_t *W; int64_t ldw;   // [N, K]  (nn.Linear weight layout)
+    bf16_t *C; int64_t ldc;         // output
+    int M, N, K;
+    int epi;
+    const bf16_t *bias;             // [N] or null
+    const bf16_t *res; int64_t ldr; // residual (may alias C)
+    const bf16_t *gate; int64_t gate_bstride; int rows_per_batch;
+};
+int gemm(const GemmArgs &a, hipStream_t s);
+
+// --------------------------------------------------------------- small ops --
+// y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16
+int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
+               int64_t ldy, int M, int N, int K, int act, hipStream_t s);
+// sinusoid of bf16(t*1000): emb[b][0:128]=cos, [128:256]=sin, as bf16 (base:225-246)
+int timestep_sinusoid(const float *t, const float *t_r, int t_stride, int use_diff, int Bc,
+                      const float *freqs, bf16_t *emb, hipStream_t s);
+// out = bf16(a + b) elementwise
+int add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *out, int64_t n, hipStream_t s);
+// mod[l][b][j][d] = bf16(table[l][j][d] + proj[b][j][d]) for all layers
+int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj, int Bc, int D,
+               bf16_t *mod, hipStream_t s);
+// proj_in input pack: X[b][s][k*192+c] = (c<128 ? ctx : xt)[b % Bx][2s+k][..] or 0
+int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
+                 hipStream_t s);
+// crop [Bc][2S][64] → [Bc][T][64]
+int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16_t *dst,
+              hipStream_t s);
+
+// ---------------------------------------------------------------- norms ----
+// out[m] = AdaLN or plain RMSNorm of x[m] (rows of D):
+//   plain: bf16(w · bf16(x·rsqrt(mean x²+eps)))
+//   mod:   bf16(bf16(plain · bf16(1+scale[b])) + shift[b])
+int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
+                int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
+                hipStream_t s);
+// per-head post-projection: q/k RMSNorm (+RoPE) and scatter to head-major layouts
+struct HeadPostArgs {
+    const bf16_t *src; int64_t ld_src;   // rows [B*S]
+    int B, S;
+    int nq, nk, nv;                      // heads of each kind in the row (q | k | v)
+    const bf16_t *qw, *kw;               // norm weights [128]
+    const bf16_t *cos, *sin;             // [S][128] bf16 or null (no RoPE)
+    bf16_t *q, *k, *v;                   // [B][nq|nk|nv][S_dst][128]
+    int S_dst;
+    float eps;
+};
+int head_post(const HeadPostArgs &a, hipStream_t s);
+
+// ------------------------------------------------------------- attention ---
+int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
+              int Sq, int Sk, int window, float scale, int64_t o_ld, hipStream_t s);
+
+// --------------------------------------------------------------- sampler ---
+int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,
+              float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s);
+int axpy_bf16(const bf16_t *vt, bf16_t *xt, int64_t n, float sc, hipStream_t s);
+
+// ----------------------------------------------------------------- misc ----
+int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s);
+
+}  // namespace acehip

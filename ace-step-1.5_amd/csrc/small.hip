@@ -1,0 +1,163 @@
+// small.hip — the DiT's small / bandwidth-trivial kernels.
+//
+// timestep embedding (reference base:225-254): the sinusoid of bf16(t·1000)
+// and the three tiny-M linears run as a weight-streaming GEMV (M = Bc ≤ 16);
+// the per-layer AdaLN tables (base:493-495) are added once per forward for all
+// layers; proj_in's concat+pad+patchify (base:1347-1358) becomes a gather
+// into the K=384 GEMM operand; proj_out's crop (base:1501) a row copy.
+#include "kernels.h"
+
+namespace acehip {
+namespace {
+
+__global__ __launch_bounds__(256) void gemv_small_kernel(const bf16_t *__restrict__ x, int64_t ldx,
+                                                         const bf16_t *__restrict__ W,
+                                                         const bf16_t *__restrict__ bias,
+                                                         bf16_t *__restrict__ y, int64_t ldy, int M,
+                                                         int N, int K, int act) {
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    float acc[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) acc[m] = 0.f;
+    const bf16_t *wr = W + (int64_t)n * K;
+    for (int k = lane * 8; k < K; k += 512) {
+        float wv[8];
+        unpack8(*(const uint4 *)(wr + k), wv);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m < M) {
+                float xv[8];
+                unpack8(*(const uint4 *)(x + m * ldx + k), xv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xx = act ? rbf(silu_f(xv[j])) : xv[j];
+                    acc[m] += wv[j] * xx;
+                }
+            }
+        }
+    }
+    const float bb = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        if (m < M) {
+            const float v = wave_sum(acc[m]);
+            if (lane == 0) y[m * ldy + n] = f2bf(v + bb);
+        }
+    }
+}
+
+__global__ void sinusoid_kernel(const float *t, const float *t_r, int t_stride, int use_diff,
+                                const float *freqs, bf16_t *emb) {
+    const int b = blockIdx.x, i = threadIdx.x;  // 128 threads
+    float tv = t[b * t_stride];
+    if (use_diff) tv = rbf(tv - t_r[b * t_stride]);   // (timestep - timestep_r) in bf16
+    const float ts = rbf(tv * 1000.0f);                // t * scale in the model dtype
+    const float arg = ts * freqs[i];
+    emb[b * 256 + i] = f2bf(cosf(arg));
+    emb[b * 256 + 128 + i] = f2bf(sinf(arg));
+}
+
+__global__ void add_kernel(const bf16_t *a, const bf16_t *b, bf16_t *o, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+// mod[l][b][j][d] = bf16(table[l][j][d] + proj[b][j % proj_rows][d])
+__global__ void modulation_kernel(const bf16_t *tables, int rows, const bf16_t *proj, int proj_rows,
+                                  int Bc, int D, bf16_t *mod) {
+    const int l = blockIdx.z, b = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)rows * D) return;
+    const int j = (int)(e / D), d = (int)(e % D);
+    const float v = bf2f(tables[(int64_t)l * rows * D + e]) +
+                    bf2f(proj[((int64_t)b * proj_rows + (j % proj_rows)) * D + d]);
+    mod[(((int64_t)l * Bc + b) * rows) * D + e] = f2bf(v);
+}
+
+// X[b][s][k*192 + c]: c < 128 → ctx[b%Bx][2s+k][c]; else xt[b%Bx][2s+k][c-128]; 0 past T
+__global__ void pack_patches_kernel(const bf16_t *xt, const bf16_t *ctx, int Bx, int T, int S,
+                                    bf16_t *X) {
+    const int row = blockIdx.x;           // b*S + s
+    const int b = row / S, s = row % S;
+    const int bb = b % Bx;
+    for (int i = threadIdx.x; i < 384 / 8; i += blockDim.x) {
+        const int k = (i * 8) / 192, c = (i * 8) % 192;
+        const int t = 2 * s + k;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (t < T) {
+            if (c < 128) v = *(const uint4 *)(ctx + ((int64_t)bb * T + t) * 128 + c);
+            else v = *(const uint4 *)(xt + ((int64_t)bb * T + t) * 64 + (c - 128));
+        }
+        *(uint4 *)(X + (int64_t)row * 384 + i * 8) = v;
+    }
+}
+
+__global__ void crop_kernel(const bf16_t *src, int rows_src, int rows_dst, int C, bf16_t *dst) {
+    const int b = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)rows_dst * C) return;
+    dst[(int64_t)b * rows_dst * C + e] = src[(int64_t)b * rows_src * C + e];
+}
+
+__global__ void cast_kernel(const float *src, bf16_t *dst, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = f2bf(src[i]);
+}
+
+}  // namespace
+
+int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
+               int64_t ldy, int M, int N, int K, int act, hipStream_t s) {
+    if (M > 16 || K % 8 || ldx % 8) return fail(-1, "gemv_small: M<=16, K%8==0 required");
+    gemv_small_kernel<<<(N + 3) / 4, 256, 0, s>>>(x, ldx, W, bias, y, ldy, M, N, K, act);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int timestep_sinusoid(const float *t, const float *t_r, int t_stride, int use_diff, int Bc,
+                      const float *freqs, bf16_t *emb, hipStream_t s) {
+    sinusoid_kernel<<<Bc, 128, 0, s>>>(t, t_r, t_stride, use_diff, freqs, emb);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *out, int64_t n, hipStream_t s) {
+    add_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, b, out, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj, int Bc, int D,
+               bf16_t *mod, hipStream_t s) {
+    // proj rows: 6 for the layer tables (proj [Bc][6][D]); 1 for norm_out (temb [Bc][D])
+    const int proj_rows = rows == 6 ? 6 : 1;
+    dim3 grid((unsigned)(((int64_t)rows * D + 255) / 256), Bc, n_tables);
+    modulation_kernel<<<grid, 256, 0, s>>>(tables, rows, proj, proj_rows, Bc, D, mod);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
+                 hipStream_t s) {
+    pack_patches_kernel<<<Bc * S, 64, 0, s>>>(xt, ctx, Bx, T, S, X);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16_t *dst,
+              hipStream_t s) {
+    dim3 grid((unsigned)(((int64_t)rows_dst * C + 255) / 256), Bc);
+    crop_kernel<<<grid, 256, 0, s>>>(src, rows_src, rows_dst, C, dst);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s) {
+    cast_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // namespace acehip

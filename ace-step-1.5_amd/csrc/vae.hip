@@ -1,0 +1,400 @@
+// vae.hip — the Oobleck VAE runtime behind acehip_vae_* (include/acehip.h).
+//
+// Replaces diffusers AutoencoderOobleck.decode/encode as called by the
+// reference handler (acestep/core/generation/handler/vae_decode_chunks.py:42,
+// vae_encode.py:65); structure per acestep/models/mlx/vae_model.py:94-230.
+// set_weight keeps raw (weight_g, weight_v) copies; finalize fuses
+// w = g·v/‖v‖ (vae_convert.py:18-34) straight into implicit-GEMM layouts.
+//
+// Decode runs untiled, one song at a time, with three activation buffers of
+// max(L·C) elements: X (raw residual stream) and two snaked buffers that
+// alternate as the k=7 conv input / k=1 conv input.  Every conv writes the
+// Snake of its output for its consumer (conv.hip), so the residual unit is
+//   y_s = snake2(conv7(x_s)) ;  x = x + conv1(y_s), x_s = snake_next(x)
+// with no separate activation passes.
+#include <map>
+#include <vector>
+
+#include "kernels.h"
+#include "conv.h"
+#include "../../include/acehip.h"
+
+using namespace acehip;
+
+namespace {
+
+struct Raw {
+    bf16_t *p = nullptr;
+    std::vector<int64_t> shape;
+};
+struct ConvL {
+    bf16_t *Wp = nullptr;
+    bf16_t *bias = nullptr;
+    int cin = 0, cout = 0, k = 0, stride = 1, transposed = 0;
+};
+struct SnakeP {
+    float *a = nullptr, *ib = nullptr;
+};
+struct ResU {
+    SnakeP s1, s2;
+    ConvL c1, c2;
+    int dil = 1;
+};
+struct DecBlk {
+    SnakeP snake;
+    ConvL convT;
+    ResU res[3];
+    int cin, cout, stride;
+};
+struct EncBlk {
+    ResU res[3];
+    SnakeP snake;
+    ConvL conv;
+    int cin, cout, stride;
+};
+
+}  // namespace
+
+struct acehip_vae {
+    int device = 0;
+    acehip_vae_cfg cfg{};
+    int hop = 1;
+    std::vector<void *> allocs;
+    std::map<std::string, Raw> raw;
+    bool finalized = false;
+    // decoder
+    ConvL dconv1;
+    std::vector<DecBlk> dec;
+    SnakeP dsnake;
+    float *dconv2_w = nullptr;  // [2][7][C]
+    // encoder
+    float *econv1_w = nullptr, *econv1_b = nullptr;  // [C][2][7], [C]
+    std::vector<EncBlk> enc;
+    SnakeP esnake;
+    ConvL econv2;
+    // buffers
+    bf16_t *X = nullptr, *P = nullptr, *Q = nullptr;
+    int64_t buf_elems = 0;
+};
+
+namespace {
+
+void *valloc(acehip_vae *h, size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+    h->allocs.push_back(p);
+    return p;
+}
+
+std::string norm_name(std::string n) {
+    const std::string o0 = ".parametrizations.weight.original0", o1 = ".parametrizations.weight.original1";
+    size_t k;
+    if ((k = n.find(o0)) != std::string::npos) n = n.substr(0, k) + ".weight_g";
+    else if ((k = n.find(o1)) != std::string::npos) n = n.substr(0, k) + ".weight_v";
+    if (n.rfind("vae.", 0) == 0) n = n.substr(4);
+    return n;
+}
+
+Raw *find(acehip_vae *h, const std::string &n) {
+    auto it = h->raw.find(n);
+    return it == h->raw.end() ? nullptr : &it->second;
+}
+
+int make_conv(acehip_vae *h, const std::string &name, int cin, int cout, int k, int stride, bool transposed,
+              bool bias, ConvL &out) {
+    Raw *v = find(h, name + ".weight_v");
+    Raw *g = find(h, name + ".weight_g");
+    if (!v) v = find(h, name + ".weight");
+    if (!v) return fail(ACEHIP_E_STATE, "vae_finalize: missing " + name + ".weight_v");
+    const int d0 = transposed ? cin : cout, d1 = transposed ? cout : cin;
+    if (v->shape != std::vector<int64_t>{d0, d1, k})
+        return fail(ACEHIP_E_ARG, "vae_finalize: bad shape for " + name);
+    out.cin = cin; out.cout = cout; out.k = k; out.stride = stride; out.transposed = transposed;
+    const size_t n = (size_t)cin * cout * k;
+    out.Wp = (bf16_t *)valloc(h, n * 2);
+    if (!out.Wp) return fail(ACEHIP_E_OOM, "vae_finalize: oom");
+    int rc = pack_conv_weight(v->p, g ? g->p : nullptr, d0, d1, k, transposed ? 1 : 0, stride, out.Wp, 0);
+    if (rc) return rc;
+    if (bias) {
+        Raw *b = find(h, name + ".bias");
+        if (!b) return fail(ACEHIP_E_STATE, "vae_finalize: missing " + name + ".bias");
+        out.bias = b->p;   // kept (raw buffer stays alive)
+    }
+    return 0;
+}
+
+int make_snake(acehip_vae *h, const std::string &name, int C, SnakeP &s) {
+    Raw *a = find(h, name + ".alpha"), *b = find(h, name + ".beta");
+    if (!a || !b) return fail(ACEHIP_E_STATE, "vae_finalize: missing " + name + ".alpha/.beta");
+    s.a = (float *)valloc(h, C * 4);
+    s.ib = (float *)valloc(h, C * 4);
+    if (!s.a || !s.ib) return fail(ACEHIP_E_OOM, "vae_finalize: oom");
+    return snake_params(a->p, b->p, C, s.a, s.ib, 0);
+}
+
+int make_res(acehip_vae *h, const std::string &p, int C, int dil, ResU &r) {
+    int rc;
+    r.dil = dil;
+    if ((rc = make_snake(h, p + ".snake1", C, r.s1))) return rc;
+    if ((rc = make_snake(h, p + ".snake2", C, r.s2))) return rc;
+    if ((rc = make_conv(h, p + ".conv1", C, C, 7, 1, false, true, r.c1))) return rc;
+    return make_conv(h, p + ".conv2", C, C, 1, 1, false, true, r.c2);
+}
+
+// one implicit-GEMM conv launch
+int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps, int dil, int a_stride,
+             int a_off, int c_stride, int c_off, int64_t L_out, bf16_t *out, bf16_t *out_s, const SnakeP *sn,
+             const bf16_t *res, int phases, hipStream_t s) {
+    ConvArgs a{};
+    a.in = in; a.L_in = L_in; a.Cin = c.cin;
+    a.W = c.Wp; a.w_pstride = (int64_t)c.cout * taps * c.cin;
+    a.bias = c.bias; a.out = out; a.out_s = out_s;
+    a.sa = sn ? sn->a : nullptr; a.sib = sn ? sn->ib : nullptr;
+    a.res = res; a.L_out = L_out; a.N = c.cout; a.M = M;
+    a.taps = taps; a.dil = dil; a.a_stride = a_stride; a.a_off = a_off; a.c_stride = c_stride; a.c_off = c_off;
+    return conv_gemm(a, phases, s);
+}
+
+// residual unit on (x raw in X, x_s in cur): leaves x in X (if keep_raw) and next-snaked x in cur
+int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, const SnakeP &next, bool keep_raw,
+             hipStream_t s) {
+    int rc;
+    if ((rc = run_conv(r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s)))
+        return rc;
+    return run_conv(r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int acehip_vae_create(int device, const acehip_vae_cfg *cfg, acehip_vae **out) {
+    if (!cfg || !out) return fail(ACEHIP_E_ARG, "vae_create: null argument");
+    if (cfg->n_blocks < 1 || cfg->n_blocks > 8 || cfg->max_T <= 0 || cfg->max_B <= 0)
+        return fail(ACEHIP_E_ARG, "vae_create: bad config");
+    if (cfg->audio_channels != 2) return fail(ACEHIP_E_ARG, "vae_create: stereo (2 channels) required");
+    HIP_TRY(hipSetDevice(device));
+    auto *h = new acehip_vae();
+    h->device = device;
+    h->cfg = *cfg;
+    const int n = cfg->n_blocks;
+    int hop = 1;
+    for (int i = 0; i < n; ++i) hop *= cfg->ratios[i];
+    h->hop = hop;
+    // decoder blocks: strides reversed, channels C·cm[n−i] → C·cm[n−i−1] with cm = [1] + multiples
+    std::vector<int> cm(n + 1);
+    cm[0] = 1;
+    for (int i = 0; i < n; ++i) cm[i + 1] = cfg->multiples[i];
+    h->dec.resize(n);
+    for (int i = 0; i < n; ++i) {
+        h->dec[i].cin = cfg->decoder_channels * cm[n - i];
+        h->dec[i].cout = cfg->decoder_channels * cm[n - i - 1];
+        h->dec[i].stride = cfg->ratios[n - 1 - i];
+    }
+    h->enc.resize(n);
+    for (int i = 0; i < n; ++i) {
+        h->enc[i].cin = cfg->encoder_hidden * cm[i];
+        h->enc[i].cout = cfg->encoder_hidden * cm[i + 1];
+        h->enc[i].stride = cfg->ratios[i];
+    }
+    // activation buffer size: max over all stages of L·C
+    int64_t mx = (int64_t)cfg->max_T * std::max(cfg->latent_channels, h->dec[0].cin);
+    int64_t L = cfg->max_T;
+    for (int i = 0; i < n; ++i) {
+        L *= h->dec[i].stride;
+        mx = std::max(mx, L * (int64_t)h->dec[i].cout);
+    }
+    if (cfg->with_encoder) {
+        int64_t Le = (int64_t)cfg->max_T * hop;
+        mx = std::max(mx, Le * (int64_t)cfg->encoder_hidden);
+        for (int i = 0; i < n; ++i) {
+            mx = std::max(mx, Le * (int64_t)h->enc[i].cin);
+            Le /= h->enc[i].stride;
+            mx = std::max(mx, Le * (int64_t)h->enc[i].cout);
+        }
+    }
+    h->buf_elems = mx;
+    h->X = (bf16_t *)valloc(h, (size_t)mx * 2);
+    h->P = (bf16_t *)valloc(h, (size_t)mx * 2);
+    h->Q = (bf16_t *)valloc(h, (size_t)mx * 2);
+    if (!h->X || !h->P || !h->Q) {
+        acehip_vae_destroy(h);
+        return fail(ACEHIP_E_OOM, "vae_create: activation buffers (" + std::to_string(3 * mx * 2 >> 20) + " MiB)");
+    }
+    *out = h;
+    return 0;
+}
+
+int acehip_vae_set_weight(acehip_vae *h, const char *name, const void *ptr, int dtype, int ndim,
+                          const int64_t *shape, int on_device) {
+    if (!h || !name || !ptr || !shape) return fail(ACEHIP_E_ARG, "vae_set_weight: null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const std::string nm = norm_name(name);
+    int64_t n = 1;
+    std::vector<int64_t> sh;
+    for (int i = 0; i < ndim; ++i) {
+        n *= shape[i];
+        sh.push_back(shape[i]);
+    }
+    // snake params [1,C,1] and weight_g [d0,1,1] are stored flat
+    Raw r;
+    r.shape = sh;
+    r.p = (bf16_t *)valloc(h, (size_t)n * 2);
+    if (!r.p) return fail(ACEHIP_E_OOM, "vae_set_weight: oom");
+    const hipMemcpyKind kd = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (dtype == ACEHIP_BF16) {
+        HIP_TRY(hipMemcpy(r.p, ptr, n * 2, kd));
+    } else if (dtype == ACEHIP_F32) {
+        float *tmp = (float *)valloc(h, (size_t)n * 4);
+        if (!tmp) return fail(ACEHIP_E_OOM, "vae_set_weight: oom");
+        HIP_TRY(hipMemcpy(tmp, ptr, n * 4, kd));
+        int rc = cast_f32_bf16(tmp, r.p, n, 0);
+        if (rc) return rc;
+        HIP_TRY(hipDeviceSynchronize());
+    } else {
+        return fail(ACEHIP_E_ARG, "vae_set_weight: dtype");
+    }
+    h->raw[nm] = r;
+    return 0;
+}
+
+int acehip_vae_finalize(acehip_vae *h) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    const auto &c = h->cfg;
+    const int n = c.n_blocks;
+    int rc;
+    if ((rc = make_conv(h, "decoder.conv1", c.latent_channels, h->dec[0].cin, 7, 1, false, true, h->dconv1))) return rc;
+    for (int j = 0; j < n; ++j) {
+        auto &b = h->dec[j];
+        const std::string p = "decoder.block." + std::to_string(j);
+        if ((rc = make_snake(h, p + ".snake1", b.cin, b.snake))) return rc;
+        if ((rc = make_conv(h, p + ".conv_t1", b.cin, b.cout, 2 * b.stride, b.stride, true, true, b.convT))) return rc;
+        const int dil[3] = {1, 3, 9};
+        for (int u = 0; u < 3; ++u)
+            if ((rc = make_res(h, p + ".res_unit" + std::to_string(u + 1), b.cout, dil[u], b.res[u]))) return rc;
+    }
+    if ((rc = make_snake(h, "decoder.snake1", c.decoder_channels, h->dsnake))) return rc;
+    {
+        Raw *v = find(h, "decoder.conv2.weight_v"), *g = find(h, "decoder.conv2.weight_g");
+        if (!v) v = find(h, "decoder.conv2.weight");
+        if (!v) return fail(ACEHIP_E_STATE, "vae_finalize: missing decoder.conv2");
+        h->dconv2_w = (float *)valloc(h, (size_t)c.audio_channels * 7 * c.decoder_channels * 4);
+        if ((rc = fuse_conv_weight_f32(v->p, g ? g->p : nullptr, c.audio_channels, c.decoder_channels, 7, 1,
+                                       h->dconv2_w, 0)))
+            return rc;
+    }
+    if (c.with_encoder) {
+        Raw *v = find(h, "encoder.conv1.weight_v"), *g = find(h, "encoder.conv1.weight_g");
+        Raw *b = find(h, "encoder.conv1.bias");
+        if (!v) v = find(h, "encoder.conv1.weight");
+        if (!v || !b) return fail(ACEHIP_E_STATE, "vae_finalize: missing encoder.conv1");
+        h->econv1_w = (float *)valloc(h, (size_t)c.encoder_hidden * c.audio_channels * 7 * 4);
+        h->econv1_b = (float *)valloc(h, (size_t)c.encoder_hidden * 4);
+        if ((rc = fuse_conv_weight_f32(v->p, g ? g->p : nullptr, c.encoder_hidden, c.audio_channels, 7, 0,
+                                       h->econv1_w, 0)))
+            return rc;
+        if ((rc = cast_bf16_f32(b->p, h->econv1_b, c.encoder_hidden, 0))) return rc;
+        for (int j = 0; j < n; ++j) {
+            auto &e = h->enc[j];
+            const std::string p = "encoder.block." + std::to_string(j);
+            const int dil[3] = {1, 3, 9};
+            for (int u = 0; u < 3; ++u)
+                if ((rc = make_res(h, p + ".res_unit" + std::to_string(u + 1), e.cin, dil[u], e.res[u]))) return rc;
+            if ((rc = make_snake(h, p + ".snake1", e.cin, e.snake))) return rc;
+            if ((rc = make_conv(h, p + ".conv1", e.cin, e.cout, 2 * e.stride, e.stride, false, true, e.conv))) return rc;
+        }
+        const int dm = h->enc[n - 1].cout;
+        if ((rc = make_snake(h, "encoder.snake1", dm, h->esnake))) return rc;
+        if ((rc = make_conv(h, "encoder.conv2", dm, c.encoder_hidden, 3, 1, false, true, h->econv2))) return rc;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    h->finalized = true;
+    return 0;
+}
+
+int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, void *stream) {
+    if (!h || !z || !wav) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized) return fail(ACEHIP_E_STATE, "vae_decode before finalize");
+    if (B <= 0 || T <= 0 || T > h->cfg.max_T) return fail(ACEHIP_E_ARG, "vae_decode: T out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels;
+    const int64_t Lout = (int64_t)T * h->hop;
+    int rc;
+    for (int b = 0; b < B; ++b) {
+        const bf16_t *zb = (const bf16_t *)z + (int64_t)b * Cz * T;
+        float *wb = (float *)wav + (int64_t)b * h->cfg.audio_channels * Lout;
+        bf16_t *X = h->X, *cur = h->P, *other = h->Q;
+        if ((rc = cf_to_nlc(zb, Cz, T, X, s))) return rc;
+        // conv1 (k7) → snaked by block 0's snake1
+        if ((rc = run_conv(h->dconv1, X, T, T, 7, 1, 1, -3, 1, 0, T, nullptr, cur, &h->dec[0].snake, nullptr, 1, s)))
+            return rc;
+        int64_t L = T;
+        for (int j = 0; j < n; ++j) {
+            const auto &bk = h->dec[j];
+            const int st = bk.stride, pad = (st + 1) / 2;
+            // ConvTranspose1d as `st` phase GEMMs → raw x (residual) + snaked x for res_unit1
+            if ((rc = run_conv(bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
+                               nullptr, st, s)))
+                return rc;
+            L *= st;
+            std::swap(cur, other);
+            for (int u = 0; u < 3; ++u) {
+                const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : (j + 1 < n ? h->dec[j + 1].snake : h->dsnake);
+                if ((rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s))) return rc;
+            }
+        }
+        if ((rc = conv_out(cur, L, h->cfg.decoder_channels, h->dconv2_w, h->cfg.audio_channels, wb, s))) return rc;
+    }
+    return 0;
+}
+
+int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *eps, void *z_out, void *stream) {
+    if (!h || !wav || !z_out) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized || !h->cfg.with_encoder) return fail(ACEHIP_E_STATE, "vae_encode: encoder not loaded");
+    if (B <= 0 || N <= 0 || N % h->hop || N / h->hop > h->cfg.max_T)
+        return fail(ACEHIP_E_ARG, "vae_encode: N must be a positive multiple of hop within max_T");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels, T = N / h->hop;
+    int rc;
+    for (int b = 0; b < B; ++b) {
+        const bf16_t *wb = (const bf16_t *)wav + (int64_t)b * h->cfg.audio_channels * N;
+        bf16_t *zb = (bf16_t *)z_out + (int64_t)b * Cz * T;
+        const bf16_t *eb = eps ? (const bf16_t *)eps + (int64_t)b * Cz * T : nullptr;
+        bf16_t *X = h->X, *cur = h->P, *other = h->Q;
+        if ((rc = conv_in(wb, N, h->cfg.audio_channels, h->econv1_w, h->econv1_b, h->cfg.encoder_hidden, X, cur,
+                          h->enc[0].res[0].s1.a, h->enc[0].res[0].s1.ib, s)))
+            return rc;
+        int64_t L = N;
+        for (int j = 0; j < n; ++j) {
+            const auto &bk = h->enc[j];
+            for (int u = 0; u < 3; ++u) {
+                const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : bk.snake;
+                if ((rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s))) return rc;
+            }
+            const int st = bk.stride, pad = (st + 1) / 2;
+            const SnakeP &next = j + 1 < n ? h->enc[j + 1].res[0].s1 : h->esnake;
+            if ((rc = run_conv(bk.conv, cur, L, L / st, 2 * st, 1, st, -pad, 1, 0, L / st, j + 1 < n ? X : nullptr,
+                               other, &next, nullptr, 1, s)))
+                return rc;
+            L /= st;
+            std::swap(cur, other);
+        }
+        // conv2 (k3, pad 1) → h [T][2·Cz] (mean | scale), then the Gaussian sample
+        if ((rc = run_conv(h->econv2, cur, L, L, 3, 1, 1, -1, 1, 0, L, X, nullptr, nullptr, nullptr, 1, s))) return rc;
+        if ((rc = gauss_sample(X, T, Cz, eb, zb, s))) return rc;
+    }
+    return 0;
+}
+
+int acehip_vae_destroy(acehip_vae *h) {
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    for (void *p : h->allocs) (void)hipFree(p);
+    delete h;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+/*
+ * acehip.h — C ABI of libacehip.so, the MI355X (gfx950) implementation of the
+ * ACE-Step 1.5 hot path: the DiT flow-matching denoise step and the Oobleck
+ * VAE decode/encode.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes. No
+ * torch types cross this boundary.  All tensors are caller-owned, contiguous,
+ * device-resident buffers (e.g. torch.Tensor.data_ptr()); the library owns the
+ * packed weights, the cross-attention K/V cache and the workspace (sized at
+ * create time from the max_* fields).  Nothing is allocated inside
+ * forward/decode/encode/sampler calls.  Work is enqueued on the caller's
+ * stream (hipStream_t passed as void*); no entry point synchronises the host.
+ *
+ * Threading: a handle is bound to one device and is not re-entrant; every
+ * entry point calls hipSetDevice(handle->device) first because callers (the
+ * reference API server's ThreadPoolExecutor, reference
+ * acestep/api_server.py:1291-1292) may call from any thread.
+ *
+ * Errors: 0 = ok; negative = error class; acehip_last_error() returns the
+ * thread-local message of the last failing call.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * the reference checkout).
+ */
+#ifndef ACEHIP_H
+#define ACEHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACEHIP_VERSION 100
+
+enum acehip_status {
+    ACEHIP_OK = 0,
+    ACEHIP_E_ARG = -1,          /* bad argument / shape */
+    ACEHIP_E_OOM = -2,          /* device allocation failed */
+    ACEHIP_E_HIP = -3,          /* HIP runtime error */
+    ACEHIP_E_STATE = -4,        /* not finalized / condition not set */
+    ACEHIP_E_NAME = -5          /* unknown weight name */
+};
+
+enum acehip_dtype { ACEHIP_F32 = 0, ACEHIP_BF16 = 1 };
+
+int acehip_get_version(void);
+const char *acehip_last_error(void);
+
+/* ---------------------------------------------------------------- DiT ---- */
+
+/* Hyper-parameters (reference AceStepConfig,
+ * acestep/models/base/configuration_acestep_v15.py:148-260). */
+typedef struct acehip_dit_cfg {
+    int hidden;          /* 2048 */
+    int intermediate;    /* 6144 */
+    int heads;           /* 16 */
+    int kv_heads;        /* 8 */
+    int head_dim;        /* 128 (the kernels require 128) */
+    int layers;          /* 24 */
+    int window;          /* 128: sliding layers attend |i-j| <= window */
+    int patch;           /* 2 */
+    int in_channels;     /* 192 = context 128 + latent 64 */
+    int out_channels;    /* 64 */
+    float eps;           /* 1e-6 */
+    float rope_theta;    /* 1e6 */
+    int max_S;           /* max tokens per batch row (T/patch) */
+    int max_Bc;          /* max DiT batch (2x songs with CFG) */
+    int max_Lenc;        /* max encoder sequence length */
+    const uint8_t *sliding; /* [layers] 1 = sliding layer; NULL = even idx */
+} acehip_dit_cfg;
+
+typedef struct acehip_dit acehip_dit;
+
+/* replaces: AutoModel.from_pretrained(...).to(device).to(dtype)
+ * (acestep/core/generation/handler/init_service_loader.py:56-89) */
+int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out);
+
+/* One reference state-dict tensor by its HF name without the "decoder."
+ * prefix (e.g. "layers.3.mlp.gate_proj.weight").  Copies and
+ * repacks; the caller keeps ownership of ptr.  dtype: ACEHIP_F32/BF16.
+ * Precedent: acestep/models/mlx/dit_convert.py:11-66. */
+int acehip_dit_set_weight(acehip_dit *h, const char *name, const void *ptr, int dtype,
+                          int ndim, const int64_t *shape, int on_device);
+
+/* Validates that every tensor is present; builds fused layouts. */
+int acehip_dit_finalize(acehip_dit *h);
+
+/* condition_embedder + per-layer cross-attention K/V cache.
+ * replaces: the first-step branch of AceStepAttention.forward
+ * (acestep/models/base/modeling_acestep_v15_base.py:310-325, :1359).
+ * enc: bf16 [Bc, Lenc, hidden] (CFG: cond rows then null rows). */
+int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, void *stream);
+
+/* One decoder forward: AceStepDiTModel.forward
+ * (acestep/models/base/modeling_acestep_v15_base.py:1303-1507).
+ * xt: bf16 [Bx, T, 64]; ctx: bf16 [Bx, T, 128]; batch row b of the DiT reads
+ * xt/ctx row (b % Bx) — CFG's cat([xt, xt]) without a copy (base:1929).
+ * t, t_r: device fp32 [Bc] holding bf16-representable values; t_stride 0
+ * broadcasts element 0.  vt_out: bf16 [Bc, T, 64]. */
+int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx,
+                       const float *t, const float *t_r, int t_stride, int Bc, int T,
+                       void *vt_out, void *stream);
+
+int acehip_dit_destroy(acehip_dit *h);
+
+/* ------------------------------------------------------------ sampler ---- */
+
+/* One base/sft CFG step: cond/uncond split + APG (momentum -0.75, norm clip
+ * 2.5 over T, float64 projection) + Euler ODE update, fused.
+ * replaces: base:1943-1979 + acestep/models/base/apg_guidance.py:5-56.
+ * vt: bf16 [2B, T, 64] (cond rows then uncond rows); xt: bf16 [B, T, 64]
+ * updated in place; ra: bf16 [B, T, 64] momentum state (first_step != 0
+ * means running_average == 0); apply_cfg == 0 → vt = cond (no momentum
+ * update), apply_cfg < 0 → no CFG (vt is [B,T,64]).  dt: bf16 value.
+ * out_mode 0: xt = bf16(xt − bf16(v·dt)) (ODE);  out_mode 1: xt = v (the
+ * guided velocity, for the caller's SDE branch, base:1968-1973). */
+int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C,
+                             float guidance, float dt, int apply_cfg, int first_step,
+                             int out_mode, void *stream);
+
+/* xt = bf16(xt - bf16(vt * s)) on [n] elements — Euler ODE (turbo:1985-1991)
+ * and the final x0 = xt - vt*t (turbo:1975-1977). */
+int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream);
+
+/* ---------------------------------------------------------------- VAE ---- */
+
+/* diffusers AutoencoderOobleck config (acestep/models/mlx/vae_model.py:251-281) */
+typedef struct acehip_vae_cfg {
+    int encoder_hidden;  /* 128 */
+    int decoder_channels;/* 128 */
+    int latent_channels; /* 64 */
+    int audio_channels;  /* 2 */
+    int n_blocks;        /* 5 */
+    int ratios[8];       /* downsampling ratios, e.g. {2,4,4,6,10} */
+    int multiples[8];    /* channel multiples, e.g. {1,2,4,8,16} */
+    int max_T;           /* max latent frames per decode */
+    int max_B;
+    int with_encoder;
+} acehip_vae_cfg;
+
+typedef struct acehip_vae acehip_vae;
+
+/* replaces: AutoencoderOobleck.from_pretrained (init_service_loader.py:123-144) */
+int acehip_vae_create(int device, const acehip_vae_cfg *cfg, acehip_vae **out);
+/* diffusers names: "decoder.block.2.res_unit1.conv1.weight_g" etc.; both the
+ * weight_g/weight_v and parametrizations.weight.original{0,1} spellings. */
+int acehip_vae_set_weight(acehip_vae *h, const char *name, const void *ptr, int dtype,
+                          int ndim, const int64_t *shape, int on_device);
+/* fuses weight_g·v/||v|| and repacks every conv into implicit-GEMM layout */
+int acehip_vae_finalize(acehip_vae *h);
+
+/* vae.decode(z).sample (acestep/core/generation/handler/vae_decode_chunks.py:42)
+ * z: bf16 [B, 64, T] → wav fp32 [B, 2, T*hop]; untiled (the decoder's
+ * receptive field is < the reference's 64-frame overlap). */
+int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, void *stream);
+
+/* vae.encode(x).latent_dist.sample() (vae_encode.py:65)
+ * wav: bf16 [B, 2, N] (N multiple of hop); eps: bf16 [B, 64, N/hop] or NULL
+ * (NULL → the mean); z_out: bf16 [B, 64, N/hop]. */
+int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *eps,
+                      void *z_out, void *stream);
+
+int acehip_vae_destroy(acehip_vae *h);
+
+/* ------------------------------------------------------------ kernels ---- */
+/* Single-kernel entry points used by the parity tests and the profiler
+ * (same code the runtimes above launch). */
+
+/* C[M,N] = A[M,K] · W[N,K]^T (+bias) — bf16 MFMA, fp32 accumulate. */
+int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
+                     int M, int N, int K, const void *bias, void *stream);
+
+/* Flash attention, head_dim 128, GQA: q [B,H,Sq,128], k/v [B,KV,Sk,128] →
+ * o [B,Sq,H*128]; window < 0 = full, else |i-j| <= window. */
+int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H,
+                          int KV, int Sq, int Sk, int window, float scale, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACEHIP_H */
