@@ -97,4 +97,4 @@ class VAEConfig:
     def tiny(cls) -> "VAEConfig":
         """Narrow VAE with the real strides (hop 1920) for fast parity tests."""
         return cls(encoder_hidden_size=128, channel_multiples=[1, 1, 1, 1, 1],
-                   decoder_channels=64, decoder_input_channels=64)
+                   decoder_channels=128, decoder_input_channels=64)

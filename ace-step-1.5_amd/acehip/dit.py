@@ -123,6 +123,22 @@ class DiTRuntime:
                                        ptr(out), stream_ptr()), "dit_forward")
         return out
 
+    PROFILE_KINDS = ["gemm_swiglu", "gemm_down", "gemm_qkv", "gemm_o", "attn_full", "attn_band",
+                     "attn_cross"]
+
+    def profile(self, enable: bool = True):
+        check(lib().acehip_dit_profile(self.h, 1 if enable else 0), "dit_profile")
+
+    def profile_read(self) -> Dict[str, tuple]:
+        """{kind: (launches, total_ms)} — call after synchronising the stream."""
+        out = {}
+        for i, k in enumerate(self.PROFILE_KINDS):
+            n, ms = _ffi.c_int(), _ffi.c_float()
+            check(lib().acehip_dit_profile_read(self.h, i, _ffi.ctypes.byref(n), _ffi.ctypes.byref(ms)),
+                  "dit_profile_read")
+            out[k] = (n.value, ms.value)
+        return out
+
     def close(self):
         if getattr(self, "h", None):
             lib().acehip_dit_destroy(self.h)

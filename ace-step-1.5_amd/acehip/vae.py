@@ -1,0 +1,121 @@
+"""Oobleck VAE backend: the ``vae.decode(z).sample`` / ``tiled_decode`` /
+``vae.encode(x).latent_dist.sample()`` seams of the reference handler
+(``acestep/core/generation/handler/vae_decode_chunks.py:42,95,119,147``,
+``vae_decode.py:16-85``, ``vae_encode.py:65``) on libacehip's implicit-GEMM
+HIP kernels.  No CPU fallback: the library must load.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import Dict, Optional
+
+import torch
+
+from . import _ffi
+from ._ffi import ACEHIP_BF16, ACEHIP_F32, check, lib, ptr, shape_arg, stream_ptr
+from .config import VAEConfig
+
+
+class OobleckBackend:
+    def __init__(self, cfg: VAEConfig, device=0, max_T: int = 15000, max_B: int = 1,
+                 with_encoder: bool = True):
+        self.cfg = cfg
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index or 0)
+        self.max_T = max_T
+        c = _ffi.VAECfg()
+        c.encoder_hidden = cfg.encoder_hidden_size
+        c.decoder_channels = cfg.decoder_channels
+        c.latent_channels = cfg.decoder_input_channels
+        c.audio_channels = cfg.audio_channels
+        c.n_blocks = len(cfg.downsampling_ratios)
+        for i, r in enumerate(cfg.downsampling_ratios):
+            c.ratios[i] = r
+        for i, m in enumerate(cfg.channel_multiples):
+            c.multiples[i] = m
+        c.max_T, c.max_B, c.with_encoder = max_T, max_B, 1 if with_encoder else 0
+        self.with_encoder = with_encoder
+        h = _ffi.c_void_p()
+        check(lib().acehip_vae_create(self.device.index, _ffi.ctypes.byref(c), _ffi.ctypes.byref(h)),
+              "vae_create")
+        self.h = h
+        self.hop = cfg.hop_length
+        self.dtype = torch.bfloat16
+
+    def load(self, weights: Dict[str, torch.Tensor]):
+        """diffusers state-dict names (weight_g/weight_v or parametrizations.*)."""
+        for k, v in weights.items():
+            if k.startswith("encoder.") and not self.with_encoder:
+                continue
+            t = v.detach().contiguous()
+            if t.dtype not in (torch.float32, torch.bfloat16):
+                t = t.float()
+            dt = ACEHIP_F32 if t.dtype == torch.float32 else ACEHIP_BF16
+            check(lib().acehip_vae_set_weight(self.h, k.encode(), ptr(t), dt, t.dim(),
+                                              shape_arg(tuple(t.shape)), 1 if t.is_cuda else 0),
+                  f"vae_set_weight({k})")
+        check(lib().acehip_vae_finalize(self.h), "vae_finalize")
+
+    # ----------------------------------------------------------------- API --
+    def decode_tensor(self, z: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """z [B, 64, T] → fp32 audio [B, 2, T·hop] (untiled)."""
+        z = z.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        B, C, T = z.shape
+        if out is None:
+            out = torch.empty(B, self.cfg.audio_channels, T * self.hop, device=self.device,
+                              dtype=torch.float32)
+        check(lib().acehip_vae_decode(self.h, ptr(z), B, T, ptr(out), stream_ptr()), "vae_decode")
+        return out
+
+    def decode(self, z: torch.Tensor):
+        """diffusers-style: ``.decode(z).sample``."""
+        return SimpleNamespace(sample=self.decode_tensor(z))
+
+    def tiled_decode(self, latents: torch.Tensor, chunk_size: Optional[int] = None,
+                     overlap: int = 64, offload_wav_to_cpu: Optional[bool] = None) -> torch.Tensor:
+        """Handler ``tiled_decode`` contract (vae_decode.py:16-85): [B,64,T] →
+        [B,2,T·hop].  The Oobleck decoder's receptive field (−8.2/+9.2 frames,
+        SURVEY §8a a19) is inside the reference's 64-frame overlap, so its
+        overlap-discard tiling equals an untiled decode; we decode untiled."""
+        wav = self.decode_tensor(latents)
+        return wav.cpu() if offload_wav_to_cpu else wav
+
+    def encode_tensor(self, wav: torch.Tensor, sample: bool = True,
+                      generator: Optional[torch.Generator] = None,
+                      eps: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """wav [B, 2, N] → latent [B, 64, N/hop] (mean + std·ε when sample)."""
+        if not self.with_encoder:
+            raise RuntimeError("acehip: VAE created without encoder")
+        wav = wav.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        B, _, N = wav.shape
+        T = N // self.hop
+        if eps is not None:
+            eps = eps.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        elif sample:
+            eps = torch.randn(B, self.cfg.decoder_input_channels, T, device=self.device,
+                              dtype=torch.bfloat16, generator=generator)
+        z = torch.empty(B, self.cfg.decoder_input_channels, T, device=self.device, dtype=torch.bfloat16)
+        check(lib().acehip_vae_encode(self.h, ptr(wav), B, N, ptr(eps), ptr(z), stream_ptr()), "vae_encode")
+        return z
+
+    def encode(self, wav: torch.Tensor):
+        """diffusers-style: ``.encode(x).latent_dist.sample()`` / ``.mode()``."""
+        be = self
+
+        class _Dist:
+            def sample(self, generator=None):
+                return be.encode_tensor(wav, sample=True, generator=generator)
+
+            def mode(self):
+                return be.encode_tensor(wav, sample=False)
+        return SimpleNamespace(latent_dist=_Dist())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().acehip_vae_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -68,6 +68,13 @@ struct acehip_dit {
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
     size_t tmp_elems = 0;
+
+    // optional per-kernel event timing (acehip_dit_profile)
+    static constexpr int NKIND = 7, NPAIR = 16384;
+    bool prof = false;
+    std::vector<hipEvent_t> ev;        // 2·NPAIR events
+    std::vector<int> ev_kind;          // kind of each recorded pair
+    int ev_used = 0;
 };
 
 namespace {
@@ -118,6 +125,18 @@ int build_rope(acehip_dit *h) {
     HIP_TRY(hipMemcpy(h->rope_cos, c.data(), c.size() * 2, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(h->rope_sin, s.data(), s.size() * 2, hipMemcpyHostToDevice));
     return 0;
+}
+
+// record an event pair around `launch` when profiling is on
+template <class F>
+int timed(acehip_dit *h, int kind, hipStream_t s, F &&launch) {
+    if (!h->prof || h->ev_used >= acehip_dit::NPAIR) return launch();
+    const int i = h->ev_used++;
+    h->ev_kind[i] = kind;
+    HIP_TRY(hipEventRecord(h->ev[2 * i], s));
+    const int rc = launch();
+    HIP_TRY(hipEventRecord(h->ev[2 * i + 1], s));
+    return rc;
 }
 
 }  // namespace
@@ -450,20 +469,22 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         GemmArgs q{};
         q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D; q.C = h->QKV; q.ldc = qd + 2 * kvd;
         q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_STORE;
-        RUN(gemm(q, s));
+        RUN(timed(h, 2, s, [&] { return gemm(q, s); }));
         HeadPostArgs hp{};
         hp.src = h->QKV; hp.ld_src = qd + 2 * kvd; hp.B = Bc; hp.S = S;
         hp.nq = H; hp.nk = KV; hp.nv = KV; hp.qw = ly.qn; hp.kw = ly.kn;
         hp.cos = h->rope_cos; hp.sin = h->rope_sin;
         hp.q = h->Qh; hp.k = h->Kh; hp.v = h->Vh; hp.S_dst = S; hp.eps = eps;
         RUN(head_post(hp, s));
-        RUN(attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S,
-                      h->sliding[l] ? h->cfg.window : -1, scale, qd, s));
+        RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
+            return attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
+                             scale, qd, s);
+        }));
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
-        RUN(gemm(o, s));
+        RUN(timed(h, 3, s, [&] { return gemm(o, s); }));
         // --- cross-attention, plain residual (base:513-526)
         RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
         GemmArgs cq{};
@@ -474,22 +495,24 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         cp.src = h->QKV; cp.ld_src = qd; cp.B = Bc; cp.S = S; cp.nq = H; cp.qw = ly.cqn;
         cp.q = h->Qh; cp.S_dst = S; cp.eps = eps;
         RUN(head_post(cp, s));
-        RUN(attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd, s));
+        RUN(timed(h, 6, s, [&] {
+            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd, s);
+        }));
         GemmArgs co{};
         co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
         co.M = M; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
-        RUN(gemm(co, s));
+        RUN(timed(h, 3, s, [&] { return gemm(co, s); }));
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533)
         RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s));
         GemmArgs gu{};
         gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
         gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;
-        RUN(gemm(gu, s));
+        RUN(timed(h, 0, s, [&] { return gemm(gu, s); }));
         GemmArgs dn{};
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
-        RUN(gemm(dn, s));
+        RUN(timed(h, 1, s, [&] { return gemm(dn, s); }));
     }
     // norm_out AdaLN + proj_out (base:1491-1501)
     RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s));
@@ -503,9 +526,41 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     return 0;
 }
 
+int acehip_dit_profile(acehip_dit *h, int enable) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    if (enable && h->ev.empty()) {
+        h->ev.resize(2 * acehip_dit::NPAIR);
+        h->ev_kind.resize(acehip_dit::NPAIR);
+        for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
+    }
+    h->prof = enable != 0;
+    h->ev_used = 0;
+    return 0;
+}
+
+int acehip_dit_profile_read(acehip_dit *h, int kind, int *launches, float *total_ms) {
+    if (!h || !launches || !total_ms) return fail(ACEHIP_E_ARG, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    int n = 0;
+    float tot = 0.f;
+    for (int i = 0; i < h->ev_used; ++i) {
+        if (h->ev_kind[i] != kind) continue;
+        float ms = 0.f;
+        HIP_TRY(hipEventSynchronize(h->ev[2 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]));
+        tot += ms;
+        ++n;
+    }
+    *launches = n;
+    *total_ms = tot;
+    return 0;
+}
+
 int acehip_dit_destroy(acehip_dit *h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);
+    for (auto &e : h->ev) (void)hipEventDestroy(e);
     for (void *p : h->allocs) (void)hipFree(p);
     delete h;
     return 0;

@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — seconds/song for ACE-Step 1.5 text2music on the HIP path.
+
+Workload (BASELINE.json configs[1]): a 240 s song
+(T = 6000 latent frames, S = 3000 tokens), base/sft schedule with 27 steps,
+shift 3, CFG guidance 7 (DiT batch Bc = 2) with APG, ODE/Euler, bf16, the
+full-size 24-layer DiT (random init, synthetic conditioning enc [1,641,2048],
+context [silence N(0,1) | ones]) followed by the full Oobleck VAE decode to
+48 kHz stereo.  One bench "step" = one song through the whole hot path
+(27 DiT forwards + 27 fused APG/Euler steps + VAE decode).
+
+Multi-GPU (``--gpus N`` under torchrun): one song per GPU per step (song-
+parallel), conditioning broadcast from rank 0 over RCCL, no
+collective inside the timed work; value = max-over-ranks time ÷ all songs.
+
+Prints ONE JSON line on rank 0.  ``roofline`` is the dominant kernel (the
+SwiGLU gate/up GEMM, 2·M·N·K algorithmic FLOPs per launch) timed with HIP
+events around every launch inside the timed region; ``cpu_baseline`` is the
+CPU oracle (PyTorch fp32) timed on this host for one full-size CFG DiT step +
+a 64-frame VAE window, extrapolated to the song.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--seconds", type=float, default=240.0)
+    p.add_argument("--infer-steps", type=int, default=27)
+    p.add_argument("--guidance", type=float, default=7.0)
+    p.add_argument("--shift", type=float, default=3.0)
+    p.add_argument("--lenc", type=int, default=641)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-vae", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(W_gpu, cfg, vae_w, vcfg, T, lenc):
+    """Time the CPU oracle (PyTorch fp32) on a bounded sample and extrapolate."""
+    from oracle import dit_oracle, vae_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    W = {k: v.detach().float().cpu() for k, v in W_gpu.items()}
+    g = torch.Generator().manual_seed(0)
+    S = (T + 1) // 2
+    Bc = 2
+    xt = torch.randn(Bc, T, 64, generator=g)
+    ctx = torch.randn(Bc, T, 128, generator=g)
+    enc = torch.randn(Bc, lenc, cfg.hidden_size, generator=g)
+    t = torch.full((Bc,), 0.75)
+    with torch.no_grad():
+        kv = dit_oracle.cross_kv(W, cfg, enc)
+        t0 = time.time()
+        dit_oracle.dit_forward(W, cfg, xt, t, t, enc, ctx, kv_cache=kv)
+        dit_s = time.time() - t0
+    del W
+    vae_s = 0.0
+    win = 64
+    if vae_w is not None:
+        Wv = {k: v.detach().float().cpu() for k, v in vae_w.items()}
+        z = torch.randn(1, 64, win, generator=g)
+        with torch.no_grad():
+            t0 = time.time()
+            vae_oracle.decode(Wv, vcfg, z)
+            vae_s = time.time() - t0
+    return {"dit_step_s": dit_s, "vae_window_s": vae_s, "threads": threads, "window": win}
+
+
+def main():
+    args = parse()
+    from acehip import distributed as D
+    from acehip.config import DiTConfig, VAEConfig
+    from acehip.dit import AceStepDiTBackend, DiTRuntime
+    from acehip.vae import OobleckBackend
+    from acehip.weights import synth_dit_weights, synth_null_condition, synth_vae_weights
+    from acehip.flops import dit_flops_per_row, vae_decoder_flops
+
+    rank, world, local = D.env_world()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    D.init(device=dev)
+
+    T = int(round(args.seconds * 25))
+    S = (T + 1) // 2
+    cfg = DiTConfig()
+    vcfg = VAEConfig()
+    do_cfg = args.guidance > 1.0
+    Bc = 2 if do_cfg else 1
+
+    # random-init weights of the real architecture, identical on every rank
+    W = synth_dit_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch")
+    null = synth_null_condition(cfg, seed=0, device=dev, dtype=torch.bfloat16, backend="torch")
+    rt = DiTRuntime(cfg, local, max_S=S, max_Bc=Bc, max_Lenc=args.lenc)
+    rt.load(W)
+    be = AceStepDiTBackend(rt, null, is_turbo=False)
+    vae = vae_w = None
+    if not args.no_vae:
+        vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=False, device=dev,
+                                  dtype=torch.bfloat16, backend="torch")
+        vae = OobleckBackend(vcfg, local, max_T=T, with_encoder=False)
+        vae.load(vae_w)
+
+    # synthetic conditioning on rank 0, broadcast over RCCL
+    g = torch.Generator(device=dev).manual_seed(1234)
+    enc = torch.randn(1, args.lenc, cfg.hidden_size, device=dev, generator=g).bfloat16()
+    ctx = torch.cat([torch.randn(1, T, 64, device=dev, generator=g),
+                     torch.ones(1, T, 64, device=dev)], dim=-1).bfloat16().contiguous()
+    D.broadcast_condition([enc, ctx])
+
+    dit_s_total = [0.0]
+    vae_s_total = [0.0]
+
+    def song(seed):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e2 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        res = be.generate_audio(encoder_hidden_states=enc, context_latents=ctx,
+                                infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance,
+                                shift=args.shift, seed=seed, infer_method="ode")
+        e1.record()
+        if vae is not None:
+            wav = vae.decode_tensor(res["target_latents"].transpose(1, 2))
+        e2.record()
+        return e0, e1, e2
+
+    for i in range(args.warmup):
+        song(10_000 + rank * 100 + i)
+    torch.cuda.synchronize()
+    rt.profile(True)
+    D.barrier(dev)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    evs = [song(rank * 1000 + i) for i in range(args.steps)]
+    torch.cuda.synchronize()
+    D.barrier(dev)
+    elapsed = time.time() - t0
+    elapsed_max = D.max_over_ranks(elapsed, dev)
+    prof = rt.profile_read()
+    rt.profile(False)
+    dit_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
+    vae_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+
+    songs = args.steps * world
+    sec_per_song = elapsed_max / songs
+    dit_flops_song = args.infer_steps * Bc * dit_flops_per_row(cfg, S, args.lenc)
+    vae_flops_song = vae_decoder_flops(vcfg, T) if vae is not None else 0.0
+    M = Bc * S
+    n_sw, ms_sw = prof["gemm_swiglu"]
+    sw_flops = 2.0 * M * (2 * cfg.intermediate_size) * cfg.hidden_size
+    sw_ms = ms_sw / max(n_sw, 1)
+    sw_tflops = sw_flops / (sw_ms * 1e-3) / 1e12 if n_sw else None
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tr = json.load(f)
+        traffic = tr.get("gemm_swiglu_hbm_bytes_per_launch")
+    except Exception:
+        pass
+    kernels = {k: {"launches": n, "avg_us": (ms / n * 1e3 if n else None)} for k, (n, ms) in prof.items()}
+
+    out = {
+        "metric": "seconds/song (240 s audio, 27 DiT steps)",
+        "value": round(sec_per_song, 4),
+        "unit": "s/song",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 2),
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random-init weights of the real architecture, random conditioning)",
+        "config": {"workload": f"text2music {args.seconds:g}s, base/sft {args.infer_steps} steps, "
+                               f"shift {args.shift:g}, CFG {args.guidance:g} + APG, DiT + VAE decode",
+                   "global_batch": songs, "seq_len": S, "latent_frames": T, "lenc": args.lenc,
+                   "parallelism": f"song-parallel x{world}"},
+        "songs_per_s": round(songs / elapsed_max, 4),
+        "dit_ms_per_song": round(dit_ms, 2),
+        "dit_ms_per_step": round(dit_ms / args.infer_steps, 3),
+        "vae_ms_per_song": round(vae_ms, 2),
+        "dit_tflops": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
+        "dit_mfma_frac": round(dit_flops_song / (dit_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "vae_tflops": round(vae_flops_song / (vae_ms * 1e-3) / 1e12, 1) if vae is not None else None,
+        "roofline": {"bound": "mfma", "kernel": "gemm_kernel<EPI_SWIGLU> (M=%d N=%d K=%d)" % (
+            M, 2 * cfg.intermediate_size, cfg.hidden_size),
+            "achieved": round(sw_tflops, 1) if sw_tflops else None, "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(sw_tflops / PEAK_BF16_TFLOPS, 4) if sw_tflops else None,
+            "avg_launch_us": round(sw_ms * 1e3, 1), "launches": n_sw, "traffic": traffic},
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(W, cfg, vae_w, vcfg, T, args.lenc)
+        n_win = math.ceil(T / cb["window"])
+        sec = cb["dit_step_s"] * args.infer_steps + cb["vae_window_s"] * n_win
+        out["cpu_baseline"] = {
+            "value": round(sec, 1), "unit": "s/song", "cores": cb["threads"], "kind": "port",
+            "sample": f"1 full-size CFG DiT step (Bc=2, S={S}) = {cb['dit_step_s']:.2f}s x {args.infer_steps} "
+                      f"+ one {cb['window']}-frame VAE decode window = {cb['vae_window_s']:.2f}s x {n_win}; "
+                      f"fp32 PyTorch-CPU oracle, extrapolated",
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,15 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx,
 
 int acehip_dit_destroy(acehip_dit *h);
 
+/* Per-kernel HIP-event timing inside acehip_dit_forward (for the bench's
+ * roofline numbers).  enable != 0 clears the counters and starts recording
+ * an event pair around every launch of the listed kernel families on the
+ * forward's stream; read after the caller synchronised that stream.
+ * kind: 0 SwiGLU gate/up GEMM, 1 down GEMM, 2 QKV GEMM, 3 O/cross-O GEMMs,
+ *       4 full self-attention, 5 band self-attention, 6 cross-attention. */
+int acehip_dit_profile(acehip_dit *h, int enable);
+int acehip_dit_profile_read(acehip_dit *h, int kind, int *launches, float *total_ms);
+
 /* ------------------------------------------------------------ sampler ---- */
 
 /* One base/sft CFG step: cond/uncond split + APG (momentum -0.75, norm clip

@@ -188,17 +188,3 @@ def dit_forward(W: Dict[str, Tensor], cfg, xt: Tensor, t: Tensor, t_r: Tensor,
     h = F.conv_transpose1d(h.transpose(1, 2), W["proj_out.1.weight"], W["proj_out.1.bias"],
                            stride=cfg.patch_size).transpose(1, 2)
     return h[:, :T]
-
-
-def dit_flops_per_row(cfg, S: int, Lenc: int) -> float:
-    """Algorithmic FLOPs of one DiT forward per batch row (SURVEY §8d formula)."""
-    D, H, KV, hd, F_, L, W_ = (cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads,
-                               cfg.head_dim, cfg.intermediate_size, cfg.num_hidden_layers,
-                               cfg.sliding_window)
-    pairs = sum(min(S - 1, i + W_) - max(0, i - W_) + 1 for i in range(S))
-    per_layer = (2 * S * (D * H * hd + 2 * D * KV * hd + H * hd * D) + 2 * S * (2 * D * H * hd)
-                 + 2 * S * 3 * D * F_ + 4 * S * Lenc * H * hd)
-    n_full = sum(1 for i in range(L) if not cfg.is_sliding(i))
-    n_band = L - n_full
-    return (L * per_layer + n_full * 4 * S * S * H * hd + n_band * 4 * pairs * H * hd
-            + 2 * S * (2 * cfg.in_channels) * D + 2 * S * D * (2 * cfg.audio_acoustic_hidden_dim))

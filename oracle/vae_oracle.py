@@ -91,15 +91,3 @@ def encode_sample(W, cfg, wav: Tensor, noise: Optional[Tensor] = None) -> Tensor
         return mean
     std = F.softplus(sc) + 1e-4
     return mean + std * noise
-
-
-def decoder_flops(cfg, T: int) -> float:
-    """Σ 2·L_out·C_in·C_out·k over the decoder convs."""
-    total = 2.0 * T * cfg.decoder_input_channels * cfg.decoder_block_channels()[0][0] * 7
-    L = T
-    for cin, cout, s in cfg.decoder_block_channels():
-        L *= s
-        total += 2.0 * L * cin * cout * 2  # ConvT k=2s, each output sees 2 taps
-        total += 3 * (2.0 * L * cout * cout * 7 + 2.0 * L * cout * cout)
-    total += 2.0 * L * cfg.decoder_channels * cfg.audio_channels * 7
-    return total

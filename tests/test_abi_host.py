@@ -1,0 +1,108 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol
+include/acehip.h declares; argument errors surface as RuntimeError (no GPU
+work is issued); host logic (schedules, song sharding) matches the reference;
+the multi-GPU song-parallel path works with gloo at world size 2."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+
+def test_header_symbols_exported():
+    from acehip import _ffi
+    hdr = open(os.path.join(REPO, "include", "acehip.h")).read()
+    declared = set(re.findall(r"\b(acehip_[a-z0-9_]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    lib = _ffi.lib()
+    missing = [s for s in sorted(declared) if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(_ffi.EXPORTS) == declared
+    assert lib.acehip_get_version() == 100
+
+
+def test_error_paths_without_gpu():
+    from acehip import _ffi
+    lib = _ffi.lib()
+    h = ctypes.c_void_p()
+    rc = lib.acehip_dit_create(0, None, ctypes.byref(h))
+    assert rc == -1 and b"null" in lib.acehip_last_error()
+    cfg = _ffi.DiTCfg(hidden=2048, intermediate=6144, heads=16, kv_heads=8, head_dim=64, layers=24,
+                      window=128, patch=2, in_channels=192, out_channels=64, eps=1e-6,
+                      rope_theta=1e6, max_S=16, max_Bc=2, max_Lenc=16)
+    rc = lib.acehip_dit_create(0, ctypes.byref(cfg), ctypes.byref(h))
+    assert rc == -1 and b"head_dim" in lib.acehip_last_error()
+    with pytest.raises(RuntimeError, match="head_dim"):
+        _ffi.check(rc, "dit_create")
+    assert lib.acehip_dit_forward(None, None, None, 1, None, None, 0, 2, 10, None, None) == -1
+    assert lib.acehip_vae_decode(None, None, 1, 1, None, None) == -1
+
+
+def test_product_has_no_oracle_import():
+    """The product package must never import the CPU oracle (no CPU fallback)."""
+    pkg = os.path.join(REPO, "ace-step-1.5_amd", "acehip")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in re.sub(r'""".*?"""', "", src, flags=re.S).replace("#", "\n#"), f
+
+
+def test_turbo_schedule_host_logic():
+    from acehip.dit import turbo_schedule
+    from oracle.sampler_oracle import turbo_schedule_list
+    for sh in (1.0, 2.0, 3.0, 2.6, 0.4):
+        assert turbo_schedule(sh) == turbo_schedule_list(sh)
+    ts = torch.tensor([0.97, 0.76, 0.5, 0.26, 0.0])
+    assert turbo_schedule(3.0, ts) == turbo_schedule_list(3.0, ts)
+
+
+def test_base_schedule_matches_oracle_cpu():
+    from acehip.dit import base_schedule
+    from oracle.sampler_oracle import base_schedule as ob
+    for n, sh in ((27, 3.0), (60, 3.0), (8, 1.0)):
+        assert torch.equal(base_schedule(n, sh, "cpu", torch.bfloat16), ob(n, sh, torch.bfloat16))
+
+
+def test_song_assignment_partitions():
+    from acehip.distributed import song_assignment
+    for world in (1, 2, 4, 8):
+        got = sorted(sum((song_assignment(16, r, world) for r in range(world)), []))
+        assert got == list(range(16))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from acehip import distributed as D
+    D.init(backend="gloo")
+    enc = torch.full((1, 5, 8), float(rank))
+    ctx = torch.full((1, 7, 4), float(rank) + 0.5)
+    if rank == 0:
+        enc = torch.arange(40, dtype=torch.float32).reshape(1, 5, 8)
+        ctx = torch.ones(1, 7, 4) * 3
+    D.broadcast_condition([enc, ctx])
+    m = D.max_over_ranks(float(rank) * 10)
+    D.barrier()
+    g = D.gather_to_rank0(torch.tensor([rank]))
+    q.put((rank, enc.sum().item(), ctx.sum().item(), m, None if g is None else [int(x) for x in g]))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_and_max():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, es, cs, m, g in res:
+        assert es == sum(range(40)) and cs == 84.0 and m == 10.0
+    assert res[0][4] == [0, 1]

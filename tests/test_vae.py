@@ -1,0 +1,91 @@
+"""Oobleck VAE: oracle structure checks (CPU) and HIP decode/encode parity vs
+the fp32 CPU oracle (GPU).  VAE parity is UNPINNED against the reference
+(diffusers AutoencoderOobleck is absent; see oracle/vae_oracle.py)."""
+import pytest
+import torch
+
+from conftest import cosine, rel_l2
+
+from acehip.config import VAEConfig
+from acehip.weights import synth_vae_weights, vae_weight_shapes
+from oracle import vae_oracle
+
+
+def test_vae_hop_and_shapes():
+    cfg = VAEConfig()
+    assert cfg.hop_length == 1920                      # conditioning_masks.py:42-43
+    assert cfg.decoder_block_channels()[0] == (2048, 1024, 10)
+    s = vae_weight_shapes(cfg)
+    assert s["decoder.conv1.weight_v"] == (2048, 64, 7)
+    assert s["decoder.block.0.conv_t1.weight_v"] == (2048, 1024, 20)   # ConvT: [in, out, k]
+    assert s["decoder.block.0.conv_t1.weight_g"] == (2048, 1, 1)       # norm over dim 0 = input ch
+    assert s["encoder.conv2.weight_v"] == (128, 2048, 3)
+
+
+def test_weight_norm_fusion_matches_torch():
+    v = torch.randn(6, 4, 3)
+    g = torch.rand(6, 1, 1) + 0.5
+    conv = torch.nn.utils.parametrizations.weight_norm(torch.nn.Conv1d(4, 6, 3), dim=0)
+    with torch.no_grad():
+        conv.parametrizations.weight.original0.copy_(g)
+        conv.parametrizations.weight.original1.copy_(v)
+    assert torch.allclose(vae_oracle.fuse_weight_norm(g, v), conv.weight, atol=1e-6)
+
+
+def test_tiny_decoder_runs_on_cpu():
+    cfg = VAEConfig.tiny()
+    W = synth_vae_weights(cfg, seed=3, mode="parity", with_encoder=True)
+    z = torch.randn(1, 64, 3)
+    wav = vae_oracle.decode(W, cfg, z)
+    assert wav.shape == (1, 2, 3 * 1920) and torch.isfinite(wav).all()
+    lat = vae_oracle.encode_sample(W, cfg, wav)
+    assert lat.shape == (1, 64, 3)
+
+
+def _hip_vae(cfg, W, dev, max_T):
+    from acehip.vae import OobleckBackend
+    be = OobleckBackend(cfg, dev.index or 0, max_T=max_T, with_encoder=True)
+    be.load({k: v.to(dev) for k, v in W.items()})
+    return be
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name,T", [("tiny", 6), ("full", 8)])
+def test_vae_decode_parity(gpu_device, cfg_name, T):
+    cfg = VAEConfig.tiny() if cfg_name == "tiny" else VAEConfig()
+    W = synth_vae_weights(cfg, seed=5, mode="parity", with_encoder=True)
+    z = torch.randn(2, 64, T, generator=torch.Generator().manual_seed(T)).bfloat16()
+    with torch.no_grad():
+        ref = vae_oracle.decode(W, cfg, z.float())
+        # calibration: the same restatement run in bf16 (what diffusers does on
+        # the GPU) vs fp32 — 7.8 % on the full config at T=8
+        spread = rel_l2(vae_oracle.decode({k: v.bfloat16() for k, v in W.items()}, cfg, z).float(), ref)
+    be = _hip_vae(cfg, W, gpu_device, max_T=16)
+    out = be.decode(z.to(gpu_device)).sample
+    torch.cuda.synchronize()
+    out = out.cpu()
+    assert out.shape == ref.shape
+    # bf16 activations through ~35 convolutions: within the bf16 spread (+1 %)
+    assert rel_l2(out, ref) <= max(0.03, spread + 0.01), (rel_l2(out, ref), spread)
+    assert cosine(out, ref) > 0.995
+    be.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name", ["tiny", "full"])
+def test_vae_encode_parity(gpu_device, cfg_name):
+    cfg = VAEConfig.tiny() if cfg_name == "tiny" else VAEConfig()
+    W = synth_vae_weights(cfg, seed=6, mode="parity", with_encoder=True)
+    g = torch.Generator().manual_seed(1)
+    T = 3
+    wav = (0.3 * torch.randn(1, 2, T * 1920, generator=g)).bfloat16()
+    eps = torch.randn(1, 64, T, generator=g).bfloat16()
+    with torch.no_grad():
+        ref_mean = vae_oracle.encode_sample(W, cfg, wav.float())
+        ref_s = vae_oracle.encode_sample(W, cfg, wav.float(), eps.float())
+    be = _hip_vae(cfg, W, gpu_device, max_T=8)
+    mean = be.encode_tensor(wav.to(gpu_device), sample=False).float().cpu()
+    smp = be.encode_tensor(wav.to(gpu_device), eps=eps).float().cpu()
+    assert rel_l2(mean, ref_mean) < 0.03, rel_l2(mean, ref_mean)
+    assert rel_l2(smp, ref_s) < 0.03
+    be.close()
