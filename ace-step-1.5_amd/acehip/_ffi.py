@@ -25,7 +25,7 @@ EXPORTS = [
     "acehip_sampler_apg_euler", "acehip_sampler_axpy",
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
     "acehip_vae_encode", "acehip_vae_destroy",
-    "acehip_gemm_bf16", "acehip_attention_bf16",
+    "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
 ]
 
 
@@ -70,6 +70,8 @@ def _declare(lib):
         "acehip_vae_encode": (c_int, [P, P, c_int, c_int, P, P, P]),
         "acehip_vae_destroy": (c_int, [P]),
         "acehip_gemm_bf16": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
+        "acehip_gemm_bf16_ex": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, c_int,
+                                        c_int, P]),
         "acehip_attention_bf16": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                           c_float, P]),
     }

@@ -587,6 +587,18 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
     return gemm(g, (hipStream_t)stream);
 }
 
+int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,
+                        int K, const void *bias, int epi, int variant, void *stream) {
+    GemmArgs g{};
+    g.A = (const bf16_t *)A; g.lda = lda; g.W = (const bf16_t *)W; g.ldw = ldw;
+    g.C = (bf16_t *)C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
+    g.bias = (const bf16_t *)bias;
+    if (epi == 2) { g.epi = EPI_RES; g.res = (const bf16_t *)C; g.ldr = ldc; }
+    else g.epi = EPI_STORE;
+    if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
+    return gemm_variant(g, variant, (hipStream_t)stream);
+}
+
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,
                           int Sq, int Sk, int window, float scale, void *stream) {
     return attention((const bf16_t *)q, (const bf16_t *)k, (const bf16_t *)v, (bf16_t *)o, B, H, KV, Sq,

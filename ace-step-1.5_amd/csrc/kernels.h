@@ -23,6 +23,7 @@ struct GemmArgs {
     const bf16_t *gate; int64_t gate_bstride; int rows_per_batch;
 };
 int gemm(const GemmArgs &a, hipStream_t s);
+int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
 
 // --------------------------------------------------------------- small ops --
 // y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16

@@ -180,6 +180,12 @@ int acehip_vae_destroy(acehip_vae *h);
 int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                      int M, int N, int K, const void *bias, void *stream);
 
+/* Same with an explicit epilogue (0 store+bias, 2 residual add into C) and
+ * tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
+ * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage) — tuning and tests. */
+int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
+                        int M, int N, int K, const void *bias, int epi, int variant, void *stream);
+
 /* Flash attention, head_dim 128, GQA: q [B,H,Sq,128], k/v [B,KV,Sk,128] →
  * o [B,Sq,H*128]; window < 0 = full, else |i-j| <= window. */
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H,

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""GEMM variant micro-benchmark on the DiT shapes (M = Bc·S = 6000 at 240 s)."""
+import os, sys, json
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
+import torch
+from acehip import _ffi as ff
+
+dev = torch.device("cuda:0")
+shapes = {"swiglu": (6000, 12288, 2048), "down": (6000, 2048, 6144), "qkv": (6000, 4096, 2048),
+          "o": (6000, 2048, 2048), "vae_k7_c128": (46080, 128, 896), "vae_k7_c512": (360000 // 4, 512, 3584)}
+variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4").split(",")]
+res = {}
+for name, (M, N, K) in shapes.items():
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.05).bfloat16()
+    ref = (A.float() @ W.float().t())
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    fl = 2.0 * M * N * K
+    row = {}
+    for v in variants:
+        if v == 3 and N % 256:
+            continue
+        def run():
+            ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, None, 0, v,
+                                                  ff.stream_ptr()))
+        run(); torch.cuda.synchronize()
+        err = float((C.float() - ref).norm() / ref.norm())
+        for _ in range(3): run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 20
+        e0.record()
+        for _ in range(n): run()
+        e1.record(); torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / n * 1e3
+        row[f"v{v}"] = {"us": round(us, 1), "tflops": round(fl / us * 1e-6, 1), "rel": round(err, 5)}
+    Wt = W.t()
+    for _ in range(3): torch.matmul(A, Wt)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20): torch.matmul(A, Wt)
+    e1.record(); torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1e3
+    row["torch(hipBLASLt)"] = {"us": round(us, 1), "tflops": round(fl / us * 1e-6, 1)}
+    res[name] = row
+    print(name, json.dumps(row), flush=True)
