@@ -12,8 +12,10 @@
 // Layout: q [B][H][Sq][128], k/v [B][KV][Sk][128] (head-major, written by
 // head_post), o token-major [B][Sq][o_ld] at column h·128.
 //
-// Structure: workgroup = 4 waves × 32 queries of one (b, head); KV tiles of
-// 64 keys staged in LDS (rows of 256 B, 16-B chunks XOR-swizzled so that the
+// Structure: workgroup = the NREP query heads of one KV head (GQA sharing)
+// × 4 waves × 32 queries; KV tiles of 64 keys, double-buffered in LDS with
+// the next tile's global loads in flight during the current tile's MFMAs
+// (register prefetch, written after the MFMAs, one barrier per tile), staged (rows of 256 B, 16-B chunks XOR-swizzled so that the
 // K row reads (ds_read_b128) and the V transposed reads (ds_read_b64_tr_b16)
 // are bank-conflict free).  Per wave, v_mfma_f32_32x32x16_bf16 computes the
 // swapped score tile Sᵀ = K·Qᵀ, so each lane owns one query row: the row
@@ -35,19 +37,26 @@ __device__ __forceinline__ int kvoff(int row, int ch) {
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
 
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restrict__ q,
-                                                           const bf16_t *__restrict__ k,
-                                                           const bf16_t *__restrict__ v,
-                                                           bf16_t *__restrict__ o, int H, int KV,
-                                                           int Sq, int Sk, int window, float sl2,
-                                                           int64_t o_ld) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * KT * 256];
-    char *ldsK = lds, *ldsV = lds + KT * 256;
+// NREP = query heads per KV head handled by one workgroup (GQA sharing:
+// each K/V tile is staged once for all NREP heads).  4 waves × 32 queries
+// per head → QB = 128 queries per head per workgroup.
+template <int NREP>
+__global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *__restrict__ q,
+                                                                  const bf16_t *__restrict__ k,
+                                                                  const bf16_t *__restrict__ v,
+                                                                  bf16_t *__restrict__ o, int H, int KV,
+                                                                  int Sq, int Sk, int window, float sl2,
+                                                                  int64_t o_ld) {
+    constexpr int NT = 256 * NREP;
+    constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
+    constexpr int CH = 2 * KT * 16 / NT;           // 16-B chunks per thread per tile (K and V)
+    __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
-    const int b = blockIdx.z, hq = blockIdx.y, kvh = hq / (H / KV);
+    const int b = blockIdx.z, kvh = blockIdx.y;
+    const int hq = kvh * NREP + (wave >> 2);
     const int qblk = blockIdx.x * QB;
-    const int q0 = qblk + wave * 32;
+    const int q0 = qblk + (wave & 3) * 32;
     const int qi = q0 + r;
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[qi][16s + 8hh .. +8]
@@ -63,6 +72,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
         kv_lo = max(0, qblk - window);
         kv_hi = min(Sk, qblk + QB + window);
     }
+    const int t_first = kv_lo / KT;
+    const int ntiles = (kv_hi + KT - 1) / KT - t_first;
+
+    // register prefetch of one K/V tile: chunk c → (K|V, row, 16-B column chunk)
+    uint4 pre[CH];
+    auto load_tile = [&](int kv0) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int c = tid + NT * i;                // 0 .. 2·64·16
+            const int isv = c >> 10, rc = c & 1023;
+            const int row = rc >> 4, ch = rc & 15, key = kv0 + row;
+            pre[i] = make_uint4(0, 0, 0, 0);
+            if (key < Sk) pre[i] = *(const uint4 *)((isv ? vp : kp) + (int64_t)key * 128 + ch * 8);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int c = tid + NT * i;
+            const int isv = c >> 10, rc = c & 1023;
+            *(uint4 *)(lds + buf * 2 * TILE + isv * TILE + kvoff(rc >> 4, rc & 15)) = pre[i];
+        }
+    };
+
     float m = NEG, l = 0.f;
     f32x16 oacc[4];
 #pragma unroll
@@ -70,23 +103,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
 #pragma unroll
         for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
 
-    for (int kv0 = (kv_lo / KT) * KT; kv0 < kv_hi; kv0 += KT) {
-        __syncthreads();
-        // stage K and V tiles: 64 rows × 16 chunks each; zero rows past Sk
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = tid + 256 * i;
-            const int row = c >> 4, ch = c & 15;
-            const int key = kv0 + row;
-            uint4 kk = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-            if (key < Sk) {
-                kk = *(const uint4 *)(kp + (int64_t)key * 128 + ch * 8);
-                vv = *(const uint4 *)(vp + (int64_t)key * 128 + ch * 8);
-            }
-            *(uint4 *)(ldsK + kvoff(row, ch)) = kk;
-            *(uint4 *)(ldsV + kvoff(row, ch)) = vv;
-        }
-        __syncthreads();
+    load_tile(t_first * KT);
+    store_tile(0);
+    __syncthreads();
+    const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    for (int it = 0; it < ntiles; ++it) {
+        const int kv0 = (t_first + it) * KT;
+        const int cur = it & 1;
+        const bool more = it + 1 < ntiles;
+        if (more) load_tile(kv0 + KT);           // in flight during this tile's MFMAs
+        const char *ldsK = lds + cur * 2 * TILE;
+        const char *ldsV = ldsK + TILE;
 
         // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
         f32x16 st[2];
@@ -100,19 +127,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
                 st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
             }
         }
-        // scale (log2 domain) + mask + running max
+        // scale (log2 domain) + mask + running max; interior tiles of full /
+        // cross attention need no mask
         float mx = NEG;
+        if (window < 0 && kv0 + KT <= Sk) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
-                bool ok = kj < Sk;
-                if (window >= 0) ok = ok && abs(qi - kj) <= window;
-                const float sv = ok ? st[t][j] * sl2 : NEG;
-                st[t][j] = sv;
-                mx = fmaxf(mx, sv);
-            }
+                for (int j = 0; j < 16; ++j) {
+                    st[t][j] *= sl2;
+                    mx = fmaxf(mx, st[t][j]);
+                }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
+                    bool ok = kj < Sk;
+                    if (window >= 0) ok = ok && abs(qi - kj) <= window;
+                    const float sv = ok ? st[t][j] * sl2 : NEG;
+                    st[t][j] = sv;
+                    mx = fmaxf(mx, sv);
+                }
+        }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mn = fmaxf(m, mx);
         const float alpha = exp2f(m - mn);
@@ -128,10 +166,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
             }
         rs += __shfl_xor(rs, 32, 64);
         l = l * alpha + rs;
+        if (__any(alpha != 1.0f)) {                  // skip the O rescale when no row's max grew
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+                for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+        }
 
         // P (bf16) as the B operand: tile t, k-step s ← registers 8s..8s+7
         bf16x8 pf[2][2];
@@ -143,7 +183,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
                 for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
 
         // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads
-        const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             const int dc = 32 * dt + 16 * (g & 1);
@@ -164,6 +203,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t *__restri
                     oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
                 }
         }
+        if (more) store_tile(cur ^ 1);             // tile it-1's buffer: every wave left it before the last barrier
+        __syncthreads();
     }
 
     if (qi >= Sq) return;
@@ -188,9 +229,17 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     if (B <= 0 || Sq <= 0) return 0;
     if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
     if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
-    dim3 grid((Sq + QB - 1) / QB, H, B);
-    attn_fwd_kernel<<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window,
-                                         scale * 1.4426950408889634f, o_ld);
+    const int nrep = H / KV;
+    const float sl2 = scale * 1.4426950408889634f;
+    if (nrep == 2) {
+        dim3 grid((Sq + QB - 1) / QB, KV, B);
+        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld);
+    } else if (nrep == 1) {
+        dim3 grid((Sq + QB - 1) / QB, KV, B);
+        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld);
+    } else {
+        return fail(-1, "attention: heads/kv_heads must be 1 or 2");
+    }
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -17,7 +17,20 @@ struct ConvArgs {
     int64_t L_out; int N;
     int64_t M;                                   // GEMM rows per phase
     int taps, dil, a_stride, a_off, c_stride, c_off;
+    const bf16_t *zero;                          // ≥ 128 B of zeros (im2col padding source)
 };
+// fused residual unit at C = 128: c1 = the k=7 conv (in = x_s, sa/sib = snake2,
+// bias = b1); then x' = x + (W2·y_s + b2), written raw into x (keep_raw) and
+// snaked (sa_next/sib_next) into out_s
+struct ResUnitArgs {
+    ConvArgs c1;
+    const bf16_t *W2, *b2;
+    bf16_t *x;
+    bf16_t *out_s;
+    const float *sa_next, *sib_next;
+    int keep_raw;
+};
+int resunit128(const ResUnitArgs &u, hipStream_t s);
 int conv_gemm(const ConvArgs &a, int phases, hipStream_t s);
 // final decoder conv: snaked NLC [L][Cin] → fp32 channels-first [Cout=2][L], k 7, no bias
 int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s);

@@ -32,9 +32,32 @@ constexpr int TILE = BM * BK * 2;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
+// A-row source for im2col staging: row m, tap → in[m·a_stride + tap·dil + a_off][ci0 + 8c]
+// (a zero page outside [0, L_in) — glds cannot write zeros, it copies them)
+__device__ __forceinline__ const bf16_t *a_src(const ConvArgs &a, int64_t m, int tap, int ci0, int c) {
+    const int64_t pos = m * a.a_stride + (int64_t)tap * a.dil + a.a_off;
+    if (m >= a.M || pos < 0 || pos >= a.L_in) return a.zero + c * 8;
+    return a.in + pos * a.Cin + ci0 + c * 8;
+}
+
+// Snake of a value already rounded to bf16: x + 1/(e^β+1e-9)·sin(e^α x)²
+// (v_sin_f32 via __sinf: |α·x| stays small for Oobleck activations, and the
+// result is rounded to bf16 anyway)
+__device__ __forceinline__ float snake1(float x, float a, float ib) {
+    const float s = __sinf(a * x);
+    return x + ib * s * s;
+}
+
+// Both operands by global_load_lds into a 2-stage ring: [A im2col rows | W rows],
+// 128-B rows, XOR-swizzled on the source address (as gemm.hip).
+struct ConvTile {
+    static constexpr int BM = 128, BN = 128, ROWS = BM + BN, STAGE = ROWS * 128;
+};
+
 template <bool RES, bool RAW, bool SN>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
-    __shared__ __attribute__((aligned(16))) char lds[4 * TILE];
+    constexpr int BM = ConvTile::BM, BN = ConvTile::BN, STAGE = ConvTile::STAGE;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int tilesN = a.N / BN;
@@ -48,39 +71,21 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     const bf16_t *Wp = a.W + (int64_t)phase * a.w_pstride;
     const int K = a.taps * a.Cin;
 
-    const bf16_t *wsrc[4];
+    // staging: 32 glds per stage (16 A + 16 W) → 8 per wave; instruction q covers rows 8q..8q+7
+    int rowq[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (wave * 4 + i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        wsrc[i] = Wp + (int64_t)(n0 + r) * K + c * 8;
-    }
-    uint4 areg[4];
-    auto load_a = [&](int k0) {
+    for (int i = 0; i < 8; ++i) rowq[i] = (wave + 4 * i) * 8 + (lane >> 3);
+    auto stage = [&](int buf, int k0) {
+        char *b = lds + buf * STAGE;
         const int tap = k0 / a.Cin, ci0 = k0 % a.Cin;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = tid + 256 * i;
-            const int row = c >> 3, ch = c & 7;
-            const int64_t m = m0 + row;
-            const int64_t pos = m * a.a_stride + (int64_t)tap * a.dil + a.a_off;
-            areg[i] = make_uint4(0, 0, 0, 0);
-            if (m < a.M && pos >= 0 && pos < a.L_in)
-                areg[i] = *(const uint4 *)(a.in + pos * a.Cin + ci0 + ch * 8);
+        for (int i = 0; i < 8; ++i) {
+            const int r = rowq[i];
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const bf16_t *src = r < BM ? a_src(a, m0 + r, tap, ci0, c)
+                                       : Wp + (int64_t)(n0 + r - BM) * K + k0 + c * 8;
+            glds16(src, b + (wave + 4 * i) * 1024);
         }
-    };
-    auto store_a = [&](int buf) {
-        char *bx = lds + buf * 2 * TILE;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = tid + 256 * i;
-            *(uint4 *)(bx + swz(c >> 3, c & 7)) = areg[i];
-        }
-    };
-    auto stage_w = [&](int buf, int k0) {
-        char *bw = lds + buf * 2 * TILE + TILE;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds16(wsrc[i] + k0, bw + (wave * 4 + i) * 1024);
     };
 
     f32x4 acc[4][4];
@@ -90,28 +95,21 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = K / BK;
-    stage_w(0, 0);
-    load_a(0);
-    store_a(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    stage(0, 0);
     const int fr = lane & 15, fc = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        const bool more = kt + 1 < nk;
-        if (more) {
-            stage_w(cur ^ 1, (kt + 1) * BK);
-            load_a((kt + 1) * BK);
-        }
-        const char *bx = lds + cur * 2 * TILE;
-        const char *bw = bx + TILE;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+        const char *b = lds + (kt & 1) * STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 xf[4], wf[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                xf[i] = *(const bf16x8 *)(bx + swz(wm * 64 + i * 16 + fr, ks * 4 + fc));
-                wf[i] = *(const bf16x8 *)(bw + swz(wn * 64 + i * 16 + fr, ks * 4 + fc));
+                xf[i] = *(const bf16x8 *)(b + swz(wm * 64 + i * 16 + fr, ks * 4 + fc));
+                wf[i] = *(const bf16x8 *)(b + swz(BM + wn * 64 + i * 16 + fr, ks * 4 + fc));
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -119,9 +117,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
         }
-        if (more) store_a(cur ^ 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
 
 #pragma unroll
@@ -146,15 +141,147 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             if constexpr (SN) {
                 const float4 sa = *(const float4 *)(a.sa + n);
                 const float4 sb = *(const float4 *)(a.sib + n);
-                const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
-                float sn[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float s = sinf(av[r] * o[r]);
-                    sn[r] = o[r] + bv[r] * s * s;
-                }
+                const float sn[4] = {snake1(o[0], sa.x, sb.x), snake1(o[1], sa.y, sb.y),
+                                     snake1(o[2], sa.z, sb.z), snake1(o[3], sa.w, sb.w)};
                 *(uint2 *)(a.out_s + row * a.N + n) = pack4(sn);
             }
+        }
+    }
+}
+
+// Fused Oobleck residual unit at C = 128 (vae_model.py:62-87):
+//   y_s = snake2(conv7_dil(x_s) + b1)            (kept in LDS, never in HBM)
+//   x'  = x + (W2·y_s + b2);  x'_s = snake_next(x')
+// One 128-position tile per block: the k=7 GEMM (K = 896) through the
+// 2-stage glds ring, its epilogue writes y_s into the swizzled LDS image of
+// the k=1 GEMM's A operand, W2 (128×128) is staged alongside, then the k=1
+// GEMM (K = 128) and the residual / next-Snake epilogue.
+template <bool RAW>
+__global__ __launch_bounds__(256, 2) void resunit128_kernel(ResUnitArgs u) {
+    constexpr int BM = 128, STAGE = ConvTile::STAGE;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    const ConvArgs &a = u.c1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int64_t tilesM = (a.M + BM - 1) / BM;
+    const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, (int)tilesM) * BM;
+    const int K = a.taps * 128;
+    int rowq[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rowq[i] = (wave + 4 * i) * 8 + (lane >> 3);
+    auto stage = [&](int buf, int k0) {
+        char *b = lds + buf * STAGE;
+        const int tap = k0 >> 7, ci0 = k0 & 127;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = rowq[i];
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const bf16_t *src = r < BM ? a_src(a, m0 + r, tap, ci0, c) : a.W + (int64_t)(r - BM) * K + k0 + c * 8;
+            glds16(src, b + (wave + 4 * i) * 1024);
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = K / BK;
+    stage(0, 0);
+    const int fr = lane & 15, fc = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+        const char *b = lds + (kt & 1) * STAGE;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 xf[4], wf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xf[i] = *(const bf16x8 *)(b + swz(wm * 64 + i * 16 + fr, ks * 4 + fc));
+                wf[i] = *(const bf16x8 *)(b + swz(BM + wn * 64 + i * 16 + fr, ks * 4 + fc));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        }
+    }
+    // all waves done reading the ring; reuse it: [y_s k 0..63 | y_s k 64..127 | W2 k 0..63 | W2 k 64..127]
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    char *ys = lds;                 // 2 × 16 KiB
+    char *w2 = lds + 2 * 16384;     // 2 × 16 KiB
+    // W2 [128][128] → 2 k-halves of [128 rows][64]: 32 glds, 8 per wave
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int qq = wave + 4 * i;        // 0..31: half = qq >> 4, rows 8(qq&15)..+7
+        const int h = qq >> 4, r = (qq & 15) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        glds16(u.W2 + (int64_t)r * 128 + h * 64 + c * 8, w2 + h * 16384 + (qq & 15) * 1024);
+    }
+    // epilogue 1: y_s = snake2(bf16(acc + b1)) → LDS (A image of the k=1 GEMM)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = wn * 64 + j * 16 + fc * 4;
+            float bb[4];
+            unpack4(*(const uint2 *)(a.bias + n), bb);
+            const float4 sa = *(const float4 *)(a.sa + n);
+            const float4 sb = *(const float4 *)(a.sib + n);
+            const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + bb[r]), sav[r], sbv[r]);
+            const int h = n >> 6, cc = (n & 63) >> 3;
+            *(uint2 *)(ys + h * 16384 + swz(row, cc) + (n & 7) * 2) = pack4(o);
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // k=1 GEMM: K = 128 = 2 halves × 2 k-steps
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 xf[4], wf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xf[i] = *(const bf16x8 *)(ys + h * 16384 + swz(wm * 64 + i * 16 + fr, ks * 4 + fc));
+                wf[i] = *(const bf16x8 *)(w2 + h * 16384 + swz(wn * 64 + i * 16 + fr, ks * 4 + fc));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        }
+    // epilogue 2: x' = x + bf16(acc + b2); raw (optional) + snake_next
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + wm * 64 + i * 16 + fr;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = wn * 64 + j * 16 + fc * 4;
+            float bb[4], rr[4], o[4];
+            unpack4(*(const uint2 *)(u.b2 + n), bb);
+            unpack4(*(const uint2 *)(u.x + m * 128 + n), rr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = rbf(rr[r] + rbf(acc[i][j][r] + bb[r]));
+            if constexpr (RAW) *(uint2 *)(u.x + m * 128 + n) = pack4(o);
+            const float4 sa = *(const float4 *)(u.sa_next + n);
+            const float4 sb = *(const float4 *)(u.sib_next + n);
+            const float sn[4] = {snake1(o[0], sa.x, sb.x), snake1(o[1], sa.y, sb.y),
+                                 snake1(o[2], sa.z, sb.z), snake1(o[3], sa.w, sb.w)};
+            *(uint2 *)(u.out_s + m * 128 + n) = pack4(sn);
         }
     }
 }
@@ -230,10 +357,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const bf16_t *__restrict__
             for (int k = 0; k < 7; ++k) acc += x[c][k] * w[(o * Cin + c) * 7 + k];
         const float v = rbf(acc);
         if (out) out[t * Cout + o] = f2bf(v);
-        if (out_s) {
-            const float s = sinf(sa[o] * v);
-            out_s[t * Cout + o] = f2bf(v + sib[o] * s * s);
-        }
+        if (out_s) out_s[t * Cout + o] = f2bf(snake1(v, sa[o], sib[o]));
     }
 }
 
@@ -342,6 +466,7 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
         return fail(-1, "conv_gemm: N%128 and Cin%64 required (N=" + std::to_string(a.N) +
                             " Cin=" + std::to_string(a.Cin) + ")");
     if (!a.out && !a.out_s) return fail(-1, "conv_gemm: no output");
+    if (!a.zero) return fail(-1, "conv_gemm: zero page");
     if (a.out_s && (!a.sa || !a.sib)) return fail(-1, "conv_gemm: snake params");
     const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
     if (tiles >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
@@ -354,6 +479,18 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
         if (raw && sn) L(false, true, true); else if (raw) L(false, true, false); else L(false, false, true);
     }
 #undef L
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int resunit128(const ResUnitArgs &u, hipStream_t s) {
+    const ConvArgs &a = u.c1;
+    if (a.Cin != 128 || a.N != 128 || a.taps != 7 || !a.zero || !a.bias || !a.sa) return fail(-1, "resunit128: args");
+    if (u.x == u.out_s || a.in == u.out_s) return fail(-1, "resunit128: out_s must not alias x / x_s");
+    const int64_t tiles = (a.M + 127) / 128;
+    if (tiles >= (1ll << 31)) return fail(-1, "resunit128: grid too large");
+    if (u.keep_raw) resunit128_kernel<true><<<(unsigned)tiles, 256, 0, s>>>(u);
+    else resunit128_kernel<false><<<(unsigned)tiles, 256, 0, s>>>(u);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -189,6 +189,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 2: return launch<128, 128, 2, 2, 3>(a, s);   // 4 waves, 3-stage ring (96 KiB)
         case 3: return launch<128, 256, 2, 4, 3>(a, s);   // 8 waves, wide N, 3-stage (144 KiB)
         case 4: return launch<256, 128, 4, 2, 2>(a, s);   // 8 waves, 2-stage (96 KiB)
+        case 5: return launch<256, 256, 2, 4, 2>(a, s);   // 8 waves, 128x64 wave tile (128 KiB)
+        case 6: return launch<192, 256, 2, 4, 2>(a, s);   // 8 waves, 96x64 wave tile (112 KiB)
         default: return fail(-1, "gemm: bad variant");
     }
 }
@@ -209,7 +211,7 @@ int gemm(const GemmArgs &a, hipStream_t s) {
     // 256x128 2-stage tile wins on the wide SwiGLU GEMM (N = 12288), the
     // 128x128 2-stage tile (2 blocks/CU) on every N <= 4096 shape
     if (v < 0) v = a.N >= 8192 ? 4 : 0;
-    if (v == 3 && a.N % 256) v = 0;
+    if ((v == 3 || v == 5 || v == 6) && a.N % 256) v = 0;
     return gemm_variant(a, v, s);
 }
 

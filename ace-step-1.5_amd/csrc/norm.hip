@@ -42,24 +42,38 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
             for (int j = 0; j < V; ++j) ss += v[i][j] * v[i][j];
         }
     }
-    ss = wave_sum(ss);
-    const float r = 1.0f / sqrtf(ss / (float)D + eps);
     const int b = row / rows_per_batch;
     const bf16_t *sh = shift ? shift + (int64_t)b * mod_bstride : nullptr;
     const bf16_t *sc = scale ? scale + (int64_t)b * mod_bstride : nullptr;
+    // issue the weight / modulation loads before the reduction (independent of it)
+    typedef __attribute__((ext_vector_type(V / 2))) uint32_t vec_t;
+    vec_t wr[MAXV], s1r[MAXV], s2r[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        if (i < nv) {
+            const int e = (i * 64 + lane) * V;
+            wr[i] = *(const vec_t *)(w + e);
+            if (sc) {
+                s1r[i] = *(const vec_t *)(sc + e);
+                s2r[i] = *(const vec_t *)(sh + e);
+            }
+        }
+    }
+    ss = wave_sum(ss);
+    const float r = 1.0f / sqrtf(ss / (float)D + eps);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         if (i < nv) {
             const int e = (i * 64 + lane) * V;
             float wv[V], o[V];
-            if constexpr (V == 8) unpack8(*(const uint4 *)(w + e), wv);
-            else unpack4(*(const uint2 *)(w + e), wv);
+            if constexpr (V == 8) unpack8(*(const uint4 *)&wr[i], wv);
+            else unpack4(*(const uint2 *)&wr[i], wv);
 #pragma unroll
             for (int j = 0; j < V; ++j) o[j] = rbf(wv[j] * rbf(v[i][j] * r));
             if (sc) {
                 float s1[V], s2[V];
-                if constexpr (V == 8) { unpack8(*(const uint4 *)(sc + e), s1); unpack8(*(const uint4 *)(sh + e), s2); }
-                else { unpack4(*(const uint2 *)(sc + e), s1); unpack4(*(const uint2 *)(sh + e), s2); }
+                if constexpr (V == 8) { unpack8(*(const uint4 *)&s1r[i], s1); unpack8(*(const uint4 *)&s2r[i], s2); }
+                else { unpack4(*(const uint2 *)&s1r[i], s1); unpack4(*(const uint2 *)&s2r[i], s2); }
 #pragma unroll
                 for (int j = 0; j < V; ++j) o[j] = rbf(o[j] * rbf(1.0f + s1[j])) + s2[j];
             }
@@ -69,24 +83,30 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
     }
 }
 
+// 16 lanes per 128-wide head (8 elements = one 16-B load each), 4 heads per
+// wave in flight; the rotate-half partner of element d is d±64 → lane ^ 8.
 __global__ __launch_bounds__(256) void head_post_kernel(HeadPostArgs a) {
-    const int row = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = lane >> 4, li = lane & 15;      // head slot within the wave, lane within the head
+    const int row = blockIdx.x;
     const int b = row / a.S, s = row % a.S;
     const int units = a.nq + a.nk + a.nv;
     const bf16_t *src = a.src + (int64_t)row * a.ld_src;
-    const int d = lane * 2;
-    float cs0 = 0, cs1 = 0, sn0 = 0, sn1 = 0;
+    const int d = li * 8;
+    float cs[8], sn[8];
     if (a.cos) {
-        const uint32_t c = *(const uint32_t *)(a.cos + (int64_t)s * 128 + d);
-        const uint32_t n = *(const uint32_t *)(a.sin + (int64_t)s * 128 + d);
-        cs0 = bf2f(c & 0xffff); cs1 = bf2f(c >> 16);
-        sn0 = bf2f(n & 0xffff); sn1 = bf2f(n >> 16);
+        unpack8(*(const uint4 *)(a.cos + (int64_t)s * 128 + d), cs);
+        unpack8(*(const uint4 *)(a.sin + (int64_t)s * 128 + d), sn);
     }
-    for (int u = wave; u < units; u += 4) {
-        const uint32_t raw = *(const uint32_t *)(src + u * 128 + d);
-        float x0 = bf2f(raw & 0xffff), x1 = bf2f(raw >> 16);
-        bf16_t *dst;
+    for (int u0 = wave * 4; u0 < units; u0 += 16) {
+        const int u = u0 + sub;
+        const bool act = u < units;
+        float x[8];
+        if (act) unpack8(*(const uint4 *)(src + u * 128 + d), x);
+        else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = 0.f;
+        bf16_t *dst = nullptr;
         const bf16_t *nw = nullptr;
         if (u < a.nq) {
             dst = a.q + (((int64_t)b * a.nq + u) * a.S_dst + s) * 128;
@@ -94,24 +114,33 @@ __global__ __launch_bounds__(256) void head_post_kernel(HeadPostArgs a) {
         } else if (u < a.nq + a.nk) {
             dst = a.k + (((int64_t)b * a.nk + (u - a.nq)) * a.S_dst + s) * 128;
             nw = a.kw;
-        } else {
+        } else if (act) {
             dst = a.v + (((int64_t)b * a.nv + (u - a.nq - a.nk)) * a.S_dst + s) * 128;
         }
+        // per-head RMSNorm over 16 lanes (all lanes shuffle; inactive ones carry zeros)
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
         if (nw) {
-            const float ss = wave_sum(x0 * x0 + x1 * x1);
             const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + a.eps);
-            const uint32_t wr = *(const uint32_t *)(nw + d);
-            x0 = rbf(bf2f(wr & 0xffff) * rbf(x0 * r));
-            x1 = rbf(bf2f(wr >> 16) * rbf(x1 * r));
-            if (a.cos) {
-                // rotate_half: out[d] = x[d]cos[d] + (d<64 ? -x[d+64] : x[d-64]) sin[d]
-                float p0 = __shfl_xor(x0, 32, 64), p1 = __shfl_xor(x1, 32, 64);
-                if (lane < 32) { p0 = -p0; p1 = -p1; }
-                x0 = rbf(x0 * cs0) + rbf(p0 * sn0);
-                x1 = rbf(x1 * cs1) + rbf(p1 * sn1);
+            float w[8];
+            unpack8(*(const uint4 *)(nw + d), w);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = rbf(w[j] * rbf(x[j] * r));
+        }
+        if (a.cos) {
+            float p[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) p[j] = __shfl_xor(x[j], 8, 64);
+            if (nw) {
+                const float sg = li < 8 ? -1.0f : 1.0f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = rbf(x[j] * cs[j]) + rbf(sg * p[j] * sn[j]);
             }
         }
-        *(uint32_t *)(dst + d) = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
+        if (act) *(uint4 *)(dst + d) = pack8(x);
     }
 }
 

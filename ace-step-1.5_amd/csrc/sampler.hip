@@ -6,82 +6,125 @@
 //   ‖ra‖₂ over T per channel → bf16; sf = min(1, bf16(2.5/‖ra‖)); v0 = bf16(ra·sf)
 //   v1 = cond/max(‖cond‖,1e-12); par = Σ(v0·v1)·v1; orth = v0 − par   (float64)
 //   vt = bf16(cond + bf16((g−1)·bf16(orth)));  xt = bf16(xt − bf16(vt·dt))
-// The norms are global per-(song, channel) reductions over T, so one 1024-
-// thread workgroup owns a song (64 channels × 16 row groups) and runs three
-// L2-resident passes with LDS reductions in between: no host sync, no extra
-// launches.  Data per song is 2.3 MB at 240 s — bandwidth-trivial.
+// The norms are global per-(song, channel) reductions over T, so one
+// thread workgroup (512 threads) owns 8 channels of one song (16-B row accesses) and runs
+// three L2-resident passes with LDS reductions in between: no host sync, no
+// extra launches, 8 workgroups per song.  2.3 MB per song at 240 s.
 #include "kernels.h"
 
 namespace acehip {
 namespace {
 
-__global__ __launch_bounds__(1024) void apg_euler_kernel(const bf16_t *__restrict__ vt,
+// grid (8 channel groups, B songs); 512 threads = 512 rows in flight, each
+// thread owns 8 consecutive channels (one 16-B access per row)
+__global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict__ vt,
                                                          bf16_t *__restrict__ xt,
                                                          bf16_t *__restrict__ ra, int B, int T,
                                                          float guidance, float dt, int apply_cfg,
                                                          int first_step, int out_mode) {
-    constexpr int C = 64, RG = 16;
-    __shared__ float s_ss[RG][C];
-    __shared__ double s_cs[RG][C];
-    __shared__ double s_dot[RG][C];
-    const int b = blockIdx.x;
-    const int c = threadIdx.x & (C - 1), rg = threadIdx.x / C;
-    const int64_t base = (int64_t)b * T * C;
+    constexpr int C = 64, CG = 8, NTH = 512, NW = NTH / 64;
+    __shared__ float s_ss[NW][CG];
+    __shared__ double s_cs[NW][CG];
+    const int cg = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t base = (int64_t)b * T * C + cg * CG;
     const bf16_t *cond = vt + base;
     const bf16_t *unc = vt + (int64_t)B * T * C + base;
     bf16_t *x = xt + base;
     if (apply_cfg <= 0) {
         // no CFG (vt is [B,T,C]) or outside the CFG interval (vt = cond)
-        for (int t = rg; t < T; t += RG) {
-            const int64_t i = (int64_t)t * C + c;
-            const float v = bf2f(cond[i]);
-            x[i] = out_mode ? cond[i] : f2bf(bf2f(x[i]) - rbf(v * dt));
+        for (int t = tid; t < T; t += NTH) {
+            const int64_t i = (int64_t)t * C;
+            float c8[8], x8[8];
+            const uint4 cr = *(const uint4 *)(cond + i);
+            if (out_mode) { *(uint4 *)(x + i) = cr; continue; }
+            unpack8(cr, c8);
+            unpack8(*(const uint4 *)(x + i), x8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x8[j] = x8[j] - rbf(c8[j] * dt);
+            *(uint4 *)(x + i) = pack8(x8);
         }
         return;
     }
     bf16_t *rab = ra + base;
-    float ss = 0.f;
-    double cs = 0.0;
-    for (int t = rg; t < T; t += RG) {
-        const int64_t i = (int64_t)t * C + c;
-        const float cv = bf2f(cond[i]);
-        const float diff = rbf(cv - bf2f(unc[i]));
-        const float r = first_step ? diff : rbf(diff + rbf(-0.75f * bf2f(rab[i])));
-        rab[i] = f2bf(r);
-        const float rr = rbf(r);
-        ss += rr * rr;
-        cs += (double)cv * (double)cv;
-    }
-    s_ss[rg][c] = ss;
-    s_cs[rg][c] = cs;
-    __syncthreads();
-    ss = 0.f;
-    cs = 0.0;
+    float ss[8];
+    double cs[8];
 #pragma unroll
-    for (int g = 0; g < RG; ++g) { ss += s_ss[g][c]; cs += s_cs[g][c]; }
-    const float nrm = rbf(sqrtf(ss));
-    const float sf = fminf(1.0f, rbf(2.5f / nrm));
-    const double denom = fmax(sqrt(cs), 1e-12);
-    double dot = 0.0;
-    for (int t = rg; t < T; t += RG) {
-        const int64_t i = (int64_t)t * C + c;
-        const double v0 = (double)rbf(bf2f(rab[i]) * sf);
-        dot += v0 * ((double)bf2f(cond[i]) / denom);
-    }
-    s_dot[rg][c] = dot;
-    __syncthreads();
-    dot = 0.0;
+    for (int j = 0; j < 8; ++j) { ss[j] = 0.f; cs[j] = 0.0; }
+    for (int t = tid; t < T; t += NTH) {
+        const int64_t i = (int64_t)t * C;
+        float c8[8], u8[8], r8[8];
+        unpack8(*(const uint4 *)(cond + i), c8);
+        unpack8(*(const uint4 *)(unc + i), u8);
+        if (!first_step) unpack8(*(const uint4 *)(rab + i), r8);
 #pragma unroll
-    for (int g = 0; g < RG; ++g) dot += s_dot[g][c];
+        for (int j = 0; j < 8; ++j) {
+            const float diff = rbf(c8[j] - u8[j]);
+            r8[j] = first_step ? diff : rbf(diff + rbf(-0.75f * r8[j]));
+            ss[j] += r8[j] * r8[j];
+            cs[j] += (double)c8[j] * (double)c8[j];
+        }
+        *(uint4 *)(rab + i) = pack8(r8);
+    }
+    // block reduction per channel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        ss[j] = wave_sum(ss[j]);
+        cs[j] = wave_sum_d(cs[j]);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s_ss[wave][j] = ss[j]; s_cs[wave][j] = cs[j]; }
+    __syncthreads();
+    float sf[8];
+    double denom[8], dot[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        float a = 0.f;
+        double c = 0.0;
+        for (int w = 0; w < NW; ++w) { a += s_ss[w][j]; c += s_cs[w][j]; }
+        const float nrm = rbf(sqrtf(a));
+        sf[j] = fminf(1.0f, rbf(2.5f / nrm));
+        denom[j] = fmax(sqrt(c), 1e-12);
+        dot[j] = 0.0;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += NTH) {
+        const int64_t i = (int64_t)t * C;
+        float c8[8], r8[8];
+        unpack8(*(const uint4 *)(cond + i), c8);
+        unpack8(*(const uint4 *)(rab + i), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot[j] += (double)rbf(r8[j] * sf[j]) * ((double)c8[j] / denom[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dot[j] = wave_sum_d(dot[j]);
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s_cs[wave][j] = dot[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        double d = 0.0;
+        for (int w = 0; w < NW; ++w) d += s_cs[w][j];
+        dot[j] = d;
+    }
     const float gm1 = guidance - 1.0f;
-    for (int t = rg; t < T; t += RG) {
-        const int64_t i = (int64_t)t * C + c;
-        const float cv = bf2f(cond[i]);
-        const double v0 = (double)rbf(bf2f(rab[i]) * sf);
-        const double v1 = (double)cv / denom;
-        const float orth = rbf((float)(v0 - dot * v1));
-        const float g = rbf(cv + rbf(gm1 * orth));
-        x[i] = out_mode ? f2bf(g) : f2bf(bf2f(x[i]) - rbf(g * dt));
+    for (int t = tid; t < T; t += NTH) {
+        const int64_t i = (int64_t)t * C;
+        float c8[8], r8[8], x8[8];
+        unpack8(*(const uint4 *)(cond + i), c8);
+        unpack8(*(const uint4 *)(rab + i), r8);
+        if (!out_mode) unpack8(*(const uint4 *)(x + i), x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const double v0 = (double)rbf(r8[j] * sf[j]);
+            const double v1 = (double)c8[j] / denom[j];
+            const float orth = rbf((float)(v0 - dot[j] * v1));
+            const float g = rbf(c8[j] + rbf(gm1 * orth));
+            x8[j] = out_mode ? g : x8[j] - rbf(g * dt);
+        }
+        *(uint4 *)(x + i) = pack8(x8);
     }
 }
 
@@ -105,7 +148,8 @@ int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, flo
               float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s) {
     if (C != 64) return fail(-1, "apg_euler: C must be 64");
     if (B <= 0 || T <= 0) return 0;
-    apg_euler_kernel<<<B, 1024, 0, s>>>(vt, xt, ra, B, T, guidance, dt, apply_cfg, first_step, out_mode);
+    apg_euler_kernel<<<dim3(C / 8, B), 512, 0, s>>>(vt, xt, ra, B, T, guidance, dt, apply_cfg, first_step,
+                                                     out_mode);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -74,6 +74,7 @@ struct acehip_vae {
     ConvL econv2;
     // buffers
     bf16_t *X = nullptr, *P = nullptr, *Q = nullptr;
+    bf16_t *zero = nullptr;     // zero page: im2col padding source
     int64_t buf_elems = 0;
 };
 
@@ -142,6 +143,8 @@ int make_res(acehip_vae *h, const std::string &p, int C, int dil, ResU &r) {
 }
 
 // one implicit-GEMM conv launch
+const bf16_t *g_zero_page = nullptr;   // set per call from the handle (single-threaded per handle)
+
 int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps, int dil, int a_stride,
              int a_off, int c_stride, int c_off, int64_t L_out, bf16_t *out, bf16_t *out_s, const SnakeP *sn,
              const bf16_t *res, int phases, hipStream_t s) {
@@ -152,6 +155,7 @@ int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps
     a.sa = sn ? sn->a : nullptr; a.sib = sn ? sn->ib : nullptr;
     a.res = res; a.L_out = L_out; a.N = c.cout; a.M = M;
     a.taps = taps; a.dil = dil; a.a_stride = a_stride; a.a_off = a_off; a.c_stride = c_stride; a.c_off = c_off;
+    a.zero = g_zero_page;
     return conv_gemm(a, phases, s);
 }
 
@@ -159,6 +163,20 @@ int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps
 int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, const SnakeP &next, bool keep_raw,
              hipStream_t s) {
     int rc;
+    if (r.c1.cin == 128) {
+        // fused k=7 → Snake → k=1 → residual; y_s never leaves LDS
+        ResUnitArgs u{};
+        ConvArgs &a = u.c1;
+        a.in = cur; a.L_in = L; a.Cin = 128; a.W = r.c1.Wp; a.bias = r.c1.bias;
+        a.sa = r.s2.a; a.sib = r.s2.ib; a.L_out = L; a.N = 128; a.M = L;
+        a.taps = 7; a.dil = r.dil; a.a_stride = 1; a.a_off = -3 * r.dil; a.c_stride = 1; a.c_off = 0;
+        a.zero = g_zero_page;
+        u.W2 = r.c2.Wp; u.b2 = r.c2.bias; u.x = X; u.out_s = other;
+        u.sa_next = next.a; u.sib_next = next.ib; u.keep_raw = keep_raw ? 1 : 0;
+        if ((rc = resunit128(u, s))) return rc;
+        // the snaked output is in `other`: copy-free hand-back by swapping roles is done by the caller
+        return 1;   // signals "output in other"
+    }
     if ((rc = run_conv(r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s)))
         return rc;
     return run_conv(r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
@@ -217,7 +235,9 @@ int acehip_vae_create(int device, const acehip_vae_cfg *cfg, acehip_vae **out) {
     h->X = (bf16_t *)valloc(h, (size_t)mx * 2);
     h->P = (bf16_t *)valloc(h, (size_t)mx * 2);
     h->Q = (bf16_t *)valloc(h, (size_t)mx * 2);
-    if (!h->X || !h->P || !h->Q) {
+    h->zero = (bf16_t *)valloc(h, 4096);
+    if (h->zero && hipMemset(h->zero, 0, 4096) != hipSuccess) h->zero = nullptr;
+    if (!h->X || !h->P || !h->Q || !h->zero) {
         acehip_vae_destroy(h);
         return fail(ACEHIP_E_OOM, "vae_create: activation buffers (" + std::to_string(3 * mx * 2 >> 20) + " MiB)");
     }
@@ -319,6 +339,7 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
     if (B <= 0 || T <= 0 || T > h->cfg.max_T) return fail(ACEHIP_E_ARG, "vae_decode: T out of range");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    g_zero_page = h->zero;
     const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels;
     const int64_t Lout = (int64_t)T * h->hop;
     int rc;
@@ -342,7 +363,9 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
             std::swap(cur, other);
             for (int u = 0; u < 3; ++u) {
                 const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : (j + 1 < n ? h->dec[j + 1].snake : h->dsnake);
-                if ((rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s))) return rc;
+                rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s);
+                if (rc == 1) std::swap(cur, other);
+                else if (rc) return rc;
             }
         }
         if ((rc = conv_out(cur, L, h->cfg.decoder_channels, h->dconv2_w, h->cfg.audio_channels, wb, s))) return rc;
@@ -357,6 +380,7 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
         return fail(ACEHIP_E_ARG, "vae_encode: N must be a positive multiple of hop within max_T");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    g_zero_page = h->zero;
     const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels, T = N / h->hop;
     int rc;
     for (int b = 0; b < B; ++b) {
@@ -372,7 +396,9 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
             const auto &bk = h->enc[j];
             for (int u = 0; u < 3; ++u) {
                 const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : bk.snake;
-                if ((rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s))) return rc;
+                rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s);
+                if (rc == 1) std::swap(cur, other);
+                else if (rc) return rc;
             }
             const int st = bk.stride, pad = (st + 1) / 2;
             const SnakeP &next = j + 1 < n ? h->enc[j + 1].res[0].s1 : h->esnake;
