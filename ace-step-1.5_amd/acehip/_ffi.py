@@ -22,7 +22,7 @@ EXPORTS = [
     "acehip_dit_create", "acehip_dit_set_weight", "acehip_dit_finalize",
     "acehip_dit_set_condition", "acehip_dit_forward", "acehip_dit_destroy",
     "acehip_dit_profile", "acehip_dit_profile_read",
-    "acehip_sampler_apg_euler", "acehip_sampler_axpy",
+    "acehip_sampler_apg_euler", "acehip_sampler_adg_euler", "acehip_sampler_axpy",
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
     "acehip_vae_encode", "acehip_vae_destroy",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
@@ -62,6 +62,7 @@ def _declare(lib):
         "acehip_dit_profile_read": (c_int, [P, c_int, POINTER(c_int), POINTER(c_float)]),
         "acehip_sampler_apg_euler": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, c_int,
                                              c_int, c_int, P]),
+        "acehip_sampler_adg_euler": (c_int, [P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_int, P]),
         "acehip_sampler_axpy": (c_int, [P, P, c_int64, c_float, P]),
         "acehip_vae_create": (c_int, [c_int, POINTER(VAECfg), POINTER(c_void_p)]),
         "acehip_vae_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),

@@ -159,6 +159,14 @@ def apg_euler_(vt, xt, ra, guidance, dt, apply_cfg, first_step, out_mode=0):
                                          stream_ptr()), "sampler_apg_euler")
 
 
+def adg_euler_(vt, xt, guidance, sigma, dt, out_mode=0):
+    """Fused CFG split + ADG + Euler (in place on xt).  vt [2B, T, 64]; with
+    out_mode=1 xt must hold the latents on entry and receives the guided v."""
+    B, T, C = xt.shape
+    check(lib().acehip_sampler_adg_euler(ptr(vt), ptr(xt), B, T, C, float(guidance), float(sigma),
+                                         float(dt), int(out_mode), stream_ptr()), "sampler_adg_euler")
+
+
 def axpy_(vt, xt, s):
     """xt = bf16(xt − bf16(vt·s)) in place."""
     check(lib().acehip_sampler_axpy(ptr(vt), ptr(xt), xt.numel(), float(s), stream_ptr()), "axpy")
@@ -280,9 +288,6 @@ class AceStepDiTBackend:
             is_covers=torch.zeros_like(is_covers), precomputed_lm_hints_25Hz=None, audio_codes=None)
 
     def generate_audio(self, **kw) -> Dict:
-        if kw.get("use_adg"):
-            raise RuntimeError("acehip: ADG guidance (use_adg=True) is not implemented; "
-                               "caller falls back to the PyTorch path")
         t0 = time.time()
         enc, _enc_mask, ctx = self._condition(kw)
         enc_nc = ctx_nc = None
@@ -317,6 +322,7 @@ class AceStepDiTBackend:
         guidance = float(kw.get("diffusion_guidance_sale", 7.0))
         shift = float(kw.get("shift", 1.0))
         method = kw.get("infer_method", "ode")
+        use_adg = bool(kw.get("use_adg", False))
         t = base_schedule(infer_steps, shift, device, dtype, kw.get("timesteps"))
         noise = prepare_noise((B, T, ctx.shape[-1] // 2), device, dtype, kw.get("seed"))
         cns = float(kw.get("cover_noise_strength", 0.0))
@@ -336,6 +342,7 @@ class AceStepDiTBackend:
         dts = (t[:-1] - t[1:]).float().tolist()                        # bf16 t_curr − t_prev
         start, end = float(kw.get("cfg_interval_start", 0.0)), float(kw.get("cfg_interval_end", 1.0))
         cfg_on = ((t[:-1] >= start) & (t[:-1] <= end)).tolist()
+        t_host = t.float().tolist()                                    # ADG sigma = t_curr
         t_dev = t.float().contiguous()
         self._set_cond(enc, do_cfg)
         ra = torch.zeros_like(xt) if do_cfg else None
@@ -348,13 +355,20 @@ class AceStepDiTBackend:
                 ctx = ctx_nc.to(device=device, dtype=dtype).contiguous()
             vt = self.rt.forward(xt, ctx, t_dev[i:i + 1])
             apply = (1 if cfg_on[i] else 0) if do_cfg else -1
+            adg = use_adg and apply == 1          # ADG replaces APG inside the CFG interval (base:1949-1964)
             if method == "sde":
-                v = torch.empty_like(xt)
-                apg_euler_(vt, v, ra, guidance, 0.0, apply, first and apply == 1, out_mode=1)
+                if adg:
+                    v = xt.clone()
+                    adg_euler_(vt, v, guidance, t_host[i], 0.0, out_mode=1)
+                else:
+                    v = torch.empty_like(xt)
+                    apg_euler_(vt, v, ra, guidance, 0.0, apply, first and apply == 1, out_mode=1)
                 tc = t[i] * torch.ones((B,), device=device, dtype=dtype)
                 x0 = xt - v * tc[:, None, None]
                 nt = 1.0 - float(i + 1) / n
                 xt = (nt * torch.randn_like(x0) + (1 - nt) * x0).contiguous()
+            elif adg:
+                adg_euler_(vt, xt, guidance, t_host[i], dts[i])
             else:
                 apg_euler_(vt, xt, ra, guidance, dts[i], apply, first and apply == 1)
             if apply == 1:

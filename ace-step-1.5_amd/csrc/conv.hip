@@ -28,7 +28,6 @@ namespace acehip {
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE = BM * BK * 2;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 

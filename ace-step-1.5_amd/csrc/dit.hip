@@ -573,6 +573,13 @@ int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, i
                      first_step, out_mode, (hipStream_t)stream);
 }
 
+int acehip_sampler_adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, float sigma,
+                             float dt, int out_mode, void *stream) {
+    if (!vt || !xt) return fail(ACEHIP_E_ARG, "null argument");
+    return adg_euler((const bf16_t *)vt, (bf16_t *)xt, B, T, C, guidance, sigma, dt, out_mode,
+                     (hipStream_t)stream);
+}
+
 int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream) {
     if (!vt || !xt) return fail(ACEHIP_E_ARG, "null argument");
     return axpy_bf16((const bf16_t *)vt, (bf16_t *)xt, n, s, (hipStream_t)stream);
@@ -594,7 +601,9 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
     g.C = (bf16_t *)C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
     g.bias = (const bf16_t *)bias;
     if (epi == 2) { g.epi = EPI_RES; g.res = (const bf16_t *)C; g.ldr = ldc; }
-    else g.epi = EPI_STORE;
+    else if (epi == 3) g.epi = EPI_SWIGLU;   // W rows packed [32 gate; 32 up] per 64-row panel, C[M][N/2]
+    else if (epi == 0) g.epi = EPI_STORE;
+    else return fail(ACEHIP_E_ARG, "gemm_ex: epilogue");
     if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
     return gemm_variant(g, variant, (hipStream_t)stream);
 }

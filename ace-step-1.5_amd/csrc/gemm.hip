@@ -20,7 +20,10 @@
 //     operand) so each lane owns 4 consecutive output columns of one row
 //     (8-byte epilogue stores; the SwiGLU pairs gate/up in registers);
 //   * block ids are remapped XCD-aware, then grouped along M so co-resident
-//     blocks share the weight panel in L2.
+//     blocks share the weight panel in L2;
+//   * the production tiles are the ping-pong kernels (gemm_pp_kernel, 256×256
+//     and 192×256, two wave groups one barrier apart so MFMA and LDS traffic
+//     overlap on every SIMD), picked per shape by gemm_pick_variant.
 #include "kernels.h"
 
 namespace acehip {
@@ -164,6 +167,217 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong variant: BM×256 tile, 8 waves as 2 groups (wr = 0/1, A rows
+// [wr·BM/2, +BM/2)) × 4 (64 columns each).  The groups run one barrier apart,
+// so on every SIMD one wave issues MFMAs while the other issues LDS reads and
+// LDS-DMA (s_setprio(1) on the MFMA side).  Per K-tile, 4 phases of
+// [ds_read · (stage) · barrier · MFMA · barrier]:
+//   phase 0  read A-half0 + B0          stage A(kt+1) → other buffer
+//   phase 1  read B1
+//   phase 2  read A-half1
+//   phase 3  (B0, B1 still in regs)     stage B(kt+2) → this buffer's B slots,
+//                                        then vmcnt(#B glds): A(kt+1) landed
+// WAR: A(kt+1) overwrites tile kt−1's A, last read (group 1, phase 2) two
+// barriers earlier; B(kt+2) overwrites tile kt's B, last read in phase 1.
+// RAW: each wave's vmcnt precedes the barrier that opens the first read of
+// the tile (barrier 8kt+8 for group 0).  Two LDS tile buffers, ~1 tile of
+// DMA lead for A and ~1.25 for B.
+template <int BM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+    constexpr int BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
+    constexpr int ROWS = BM + BN, BUF = ROWS * 128;
+    constexpr int NA = BM / 64, NB = BN / 64;                // glds per wave for A / B of one K-tile
+    static_assert(SM % 2 == 0, "A half must be whole 16-row sub-tiles");
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
+    const int nwg = tilesM * tilesN;
+    const int wg = xcd_remap(blockIdx.x, nwg);
+    const int per_group = GROUP_M * tilesN;
+    const int gid = wg / per_group, first_m = gid * GROUP_M;
+    const int gsz = min(tilesM - first_m, GROUP_M);
+    const int tm = first_m + (wg % per_group) % gsz;
+    const int tn = (wg % per_group) / gsz;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const bf16_t *srcA[NA], *srcB[NB];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const int r = (wave + 8 * i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        srcA[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int r = (wave + 8 * i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (((BM + r) >> 1) & 7);
+        srcB[i] = a.W + (int64_t)(n0 + r) * a.ldw + c * 8;
+    }
+    auto stageA = [&](int buf, int k0) {
+        char *b = lds + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) glds16(srcA[i] + k0, b + (wave + 8 * i) * 1024);
+    };
+    auto stageB = [&](int buf, int k0) {
+        char *b = lds + buf * BUF + BM * 128;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) glds16(srcB[i] + k0, b + (wave + 8 * i) * 1024);
+    };
+    auto bar = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    f32x4 acc[SM][4];
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fc = lane >> 4;
+    const int arow = wr * TM, brow = BM + wc * 64;
+    bf16x8 xa[SMH][2], b0[2][2], b1[2][2];
+    auto readA = [&](const char *b, int h) {
+#pragma unroll
+        for (int i = 0; i < SMH; ++i)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                xa[i][ks] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
+    };
+    auto readB = [&](const char *b, int q, bf16x8 (&f)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                f[j][ks] = *(const bf16x8 *)(b + swz(brow + (q * 2 + j) * 16 + fr, ks * 4 + fc));
+    };
+    auto mma = [&](int h, int q, const bf16x8 (&f)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < SMH; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[h * SMH + i][q * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[j][ks], xa[i][ks], acc[h * SMH + i][q * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    const int nk = a.K / BK;
+    // prologue: tile 0 complete, B(1) in flight
+    stageB(0, 0);
+    stageA(0, 0);
+    if (nk > 1) {
+        stageB(1, BK);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    if (wr == 1) bar();   // group 1 runs one barrier behind
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const char *b = lds + (kt & 1) * BUF;
+        // phase 0
+        readB(b, 0, b0);
+        readA(b, 0);
+        if (kt + 1 < nk) stageA((kt + 1) & 1, (kt + 1) * BK);
+        bar();
+        mma(0, 0, b0);
+        bar();
+        // phase 1
+        readB(b, 1, b1);
+        bar();
+        mma(0, 1, b1);
+        bar();
+        // phase 2
+        readA(b, 1);
+        bar();
+        mma(1, 1, b1);
+        bar();
+        // phase 3
+        if (kt + 2 < nk) {
+            stageB(kt & 1, (kt + 2) * BK);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        mma(1, 0, b0);
+        bar();
+    }
+    if (wr == 0) bar();   // balance the barrier count
+
+    // epilogue: lane owns row m, columns n..n+3 of each 16x16 sub-tile
+#pragma unroll
+    for (int i = 0; i < SM; ++i) {
+        const int m = m0 + arow + i * 16 + fr;
+        if (m >= a.M) continue;
+        if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int nout = ((n0 + wc * 64) >> 1) + j * 16 + fc * 4;
+                float o[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float g = rbf(acc[i][j][r]);
+                    const float u = rbf(acc[i][j + 2][r]);
+                    o[r] = rbf(silu_f(g)) * u;
+                }
+                *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
+            }
+        } else {
+            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + wc * 64 + j * 16 + fc * 4;
+                float o[4];
+                if constexpr (EPI == EPI_STORE) {
+                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + bb[r];
+                } else {
+                    float rr[4];
+                    unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + n), rr);
+                    if constexpr (EPI == EPI_GATED_RES) {
+                        float gg[4];
+                        unpack4(*(const uint2 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[i][j][r]) * gg[r]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[i][j][r]);
+                    }
+                }
+                *(uint2 *)(a.C + (int64_t)m * a.ldc + n) = pack4(o);
+            }
+        }
+    }
+}
+
+template <int BM>
+int launch_pp(const GemmArgs &a, hipStream_t s) {
+    if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
+    const int tiles = ((a.M + BM - 1) / BM) * (a.N / 256);
+    switch (a.epi) {
+        case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_SWIGLU: gemm_pp_kernel<BM, EPI_SWIGLU><<<tiles, 512, 0, s>>>(a); break;
+        default: return fail(-1, "gemm: bad epilogue");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES>
 int launch(const GemmArgs &a, hipStream_t s) {
     if (a.N % BN) return fail(-1, "gemm: N not a multiple of the tile");
@@ -191,12 +405,39 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 4: return launch<256, 128, 4, 2, 2>(a, s);   // 8 waves, 2-stage (96 KiB)
         case 5: return launch<256, 256, 2, 4, 2>(a, s);   // 8 waves, 128x64 wave tile (128 KiB)
         case 6: return launch<192, 256, 2, 4, 2>(a, s);   // 8 waves, 96x64 wave tile (112 KiB)
+        case 7: return launch_pp<256>(a, s);              // ping-pong 256x256 (128 KiB)
+        case 8: return launch_pp<192>(a, s);              // ping-pong 192x256 (112 KiB)
         default: return fail(-1, "gemm: bad variant");
     }
 }
 
 static int g_variant_override = -1;
 void gemm_set_variant(int v) { g_variant_override = v; }
+
+static int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+// Tile choice from a one-block-per-CU cost model fitted on MI355X
+// (tools/bench_gemm.py): time ∝ ⌈tiles / CUs⌉ × per-tile time, with a 256×256
+// ping-pong tile costing 1.093× a 192×256 one (it does 1.33× the work).  The
+// model reproduces the measured v7/v8 ratios on all four DiT shapes to 2 %.
+// Grids too small to fill half the chip fall back to 128×128 (2 blocks/CU).
+int gemm_pick_variant(int64_t M, int N) {
+    if (N % 256) return 0;
+    const int cus = num_cus();
+    const int64_t t7 = ((M + 255) / 256) * (N / 256), t8 = ((M + 191) / 192) * (N / 256);
+    if (t8 < cus / 2) return 0;
+    const double c7 = (double)((t7 + cus - 1) / cus) * 1.093, c8 = (double)((t8 + cus - 1) / cus);
+    return c7 < c8 ? 7 : 8;
+}
 
 int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.M <= 0) return 0;
@@ -207,11 +448,8 @@ int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.epi == EPI_GATED_RES && (!a.gate || a.rows_per_batch <= 0)) return fail(-1, "gemm: gate");
     if ((a.epi == EPI_GATED_RES || a.epi == EPI_RES) && !a.res) return fail(-1, "gemm: res");
     int v = g_variant_override;
-    // measured on MI355X (tools/bench_gemm.py, uniform random operands): the
-    // 256x128 2-stage tile wins on the wide SwiGLU GEMM (N = 12288), the
-    // 128x128 2-stage tile (2 blocks/CU) on every N <= 4096 shape
-    if (v < 0) v = a.N >= 8192 ? 4 : 0;
-    if ((v == 3 || v == 5 || v == 6) && a.N % 256) v = 0;
+    if (v < 0) v = gemm_pick_variant(a.M, a.N);
+    if ((v == 3 || v >= 5) && a.N % 256) v = 0;
     return gemm_variant(a, v, s);
 }
 

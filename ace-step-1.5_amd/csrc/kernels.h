@@ -72,6 +72,8 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
 int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,
               float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s);
 int axpy_bf16(const bf16_t *vt, bf16_t *xt, int64_t n, float sc, hipStream_t s);
+int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance, float sigma,
+              float dt, int out_mode, hipStream_t s);
 
 // ----------------------------------------------------------------- misc ----
 int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s);

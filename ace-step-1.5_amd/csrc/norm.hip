@@ -16,7 +16,7 @@
 namespace acehip {
 namespace {
 
-template <int V>   // elements per vector access (8 → 16 B, 4 → 8 B)
+template <int V, int NV>   // elements per vector access (8 → 16 B, 4 → 8 B); vectors per lane (D = 64·V·NV)
 __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restrict__ x,
                                                           const bf16_t *__restrict__ w,
                                                           const bf16_t *__restrict__ shift,
@@ -28,9 +28,9 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     const bf16_t *xr = x + (int64_t)row * D;
-    constexpr int MAXV = 64 / V;  // up to D=4096
+    constexpr int MAXV = NV;
     float v[MAXV][V];
-    const int nv = D / (64 * V);
+    constexpr int nv = NV;
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
@@ -153,12 +153,33 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
     if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
     if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
     const int grid = (M + 3) / 4;
-    if (D % 512 == 0)
-        rmsnorm_mod_kernel<8><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride,
-                                                   rows_per_batch > 0 ? rows_per_batch : M, out, M, D, eps);
-    else
-        rmsnorm_mod_kernel<4><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride,
-                                                   rows_per_batch > 0 ? rows_per_batch : M, out, M, D, eps);
+    const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
+#define RMS_LAUNCH(V_, NV_)                                                                        \
+    rmsnorm_mod_kernel<V_, NV_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps)
+    if (D % 512 == 0) {
+        switch (D / 512) {
+            case 1: RMS_LAUNCH(8, 1); break;
+            case 2: RMS_LAUNCH(8, 2); break;
+            case 3: RMS_LAUNCH(8, 3); break;
+            case 4: RMS_LAUNCH(8, 4); break;
+            case 5: RMS_LAUNCH(8, 5); break;
+            case 6: RMS_LAUNCH(8, 6); break;
+            case 7: RMS_LAUNCH(8, 7); break;
+            default: RMS_LAUNCH(8, 8); break;
+        }
+    } else {
+        switch (D / 256) {
+            case 1: RMS_LAUNCH(4, 1); break;
+            case 3: RMS_LAUNCH(4, 3); break;
+            case 5: RMS_LAUNCH(4, 5); break;
+            case 7: RMS_LAUNCH(4, 7); break;
+            case 9: RMS_LAUNCH(4, 9); break;
+            case 11: RMS_LAUNCH(4, 11); break;
+            case 13: RMS_LAUNCH(4, 13); break;
+            default: RMS_LAUNCH(4, 15); break;
+        }
+    }
+#undef RMS_LAUNCH
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -142,7 +142,63 @@ __global__ void axpy_kernel(const bf16_t *vt, bf16_t *xt, int64_t n, float sc) {
     }
 }
 
+
+// ADG (Angle-based Dynamic Guidance, apg_guidance.py:107-180, apply_norm =
+// False, apply_clip = True) fused with the Euler update.  Row-local over the
+// 64 channels: one wave per (song, frame) row, lane = channel.  Precision
+// chain of the reference: hats / diff in bf16; the angle in float64
+// (call_cos_tensor on .to(float): per-element divide by the norm, then the
+// dot); the perpendicular split in float32; the recombination in float64
+// (masks applied by multiplication, so a 0/0 stays NaN exactly as in torch);
+// the result cast float64 → float32 → bf16 (c10's double → BFloat16 path).
+__global__ __launch_bounds__(256) void adg_euler_kernel(const bf16_t *__restrict__ vt,
+                                                        bf16_t *__restrict__ xt, int B, int T,
+                                                        float guidance, float sigma, float dt,
+                                                        int out_mode) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= (int64_t)B * T) return;
+    const int64_t i = row * 64 + lane;
+    const float x = bf2f(xt[i]);
+    const float vc = bf2f(vt[i]);
+    const float vu = bf2f(vt[(int64_t)B * T * 64 + i]);
+    const float ht = rbf(x - rbf(sigma * vc));
+    const float hu = rbf(x - rbf(sigma * vu));
+    const float diff = rbf(ht - hu);
+    // angle, float64
+    const double na = sqrt(wave_sum_d((double)ht * (double)ht));
+    const double nb = sqrt(wave_sum_d((double)hu * (double)hu));
+    const double cs = wave_sum_d(((double)ht / na) * ((double)hu / nb));
+    double w = (double)guidance - 1.0;
+    w = w * (w > 0.0 ? 1.0 : 0.0) + 1e-3;
+    const double clip = 3.14 / 6;
+    const double th = acos(cs);
+    const double thn = fmin(fmax(w * th, -clip), clip);
+    // perpendicular component, float32
+    const float dot = wave_sum(diff * hu);
+    const float nsq = wave_sum(hu * hu);
+    const float perp = diff - (dot / (nsq + 1e-8f)) * hu;
+    // recombination, float64
+    const double st = sin(th), sn = sin(thn);
+    const double v_new = cos(thn) * (double)ht;
+    const double p1 = (double)perp * sn / st * (st > 1e-3 ? 1.0 : 0.0);
+    const float p2 = perp * (float)w * (st <= 1e-3 ? 1.0f : 0.0f);
+    const double nw = v_new + (p1 + (double)p2);
+    const float v = rbf((float)(((double)x - nw) / (double)sigma));
+    xt[i] = f2bf(out_mode ? v : x - rbf(v * dt));
+}
+
 }  // namespace
+
+int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance, float sigma,
+              float dt, int out_mode, hipStream_t s) {
+    if (C != 64) return fail(-1, "adg_euler: C must be 64");
+    if (B <= 0 || T <= 0) return 0;
+    const int64_t rows = (int64_t)B * T;
+    adg_euler_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(vt, xt, B, T, guidance, sigma, dt, out_mode);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,
               float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s) {

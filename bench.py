@@ -173,7 +173,8 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tr = json.load(f)
-        traffic = tr.get("gemm_swiglu_hbm_bytes_per_launch")
+        if tr.get("gemm_swiglu_M") == M:          # measured on this exact GEMM shape
+            traffic = tr.get("gemm_swiglu_hbm_bytes_per_launch")
     except Exception:
         pass
     kernels = {k: {"launches": n, "avg_us": (ms / n * 1e3 if n else None)} for k, (n, ms) in prof.items()}

@@ -128,6 +128,15 @@ int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, i
                              float guidance, float dt, int apply_cfg, int first_step,
                              int out_mode, void *stream);
 
+/* One base/sft CFG step with ADG guidance (use_adg=True) + Euler, fused.
+ * replaces: base:1958-1964 + adg_forward (apg_guidance.py:107-180, angle clip
+ * pi/6, no norm).  vt: bf16 [2B, T, 64] cond then uncond; xt: bf16 [B, T, 64]
+ * updated in place; sigma: t_curr (bf16 value).  Row-local (no reduction over
+ * T).  The reference only supports B == 1 (its [N*T,1] x [N,T,C] broadcast);
+ * this computes the per-row generalisation for any B.  out_mode as above. */
+int acehip_sampler_adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance,
+                             float sigma, float dt, int out_mode, void *stream);
+
 /* xt = bf16(xt - bf16(vt * s)) on [n] elements — Euler ODE (turbo:1985-1991)
  * and the final x0 = xt - vt*t (turbo:1975-1977). */
 int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream);
@@ -180,9 +189,12 @@ int acehip_vae_destroy(acehip_vae *h);
 int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                      int M, int N, int K, const void *bias, void *stream);
 
-/* Same with an explicit epilogue (0 store+bias, 2 residual add into C) and
- * tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
- * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage) — tuning and tests. */
+/* Same with an explicit epilogue (0 store+bias, 2 residual add into C,
+ * 3 SwiGLU: W rows packed [32 gate; 32 up] per 64-row panel, C is [M][N/2])
+ * and tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
+ * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage, 5: 256x256 2-stage,
+ * 6: 192x256 2-stage, 7: 256x256 ping-pong, 8: 192x256 ping-pong; 3 and 5-8
+ * need N % 256 == 0) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 

@@ -93,14 +93,49 @@ def apg(pred_cond: Tensor, pred_uncond: Tensor, guidance_scale: float,
     return pred_cond + (guidance_scale - 1) * upd
 
 
+def adg(latents: Tensor, cond: Tensor, uncond: Tensor, sigma: Tensor, guidance_scale: float,
+        angle_clip: float = 3.14 / 6) -> Tensor:
+    """adg_forward (apg_guidance.py:107-180, apply_norm=False, apply_clip=True)
+    with its dtype chain: hats in the activation dtype, the angle in float64
+    (call_cos_tensor :63-77 on ``.to(float)``), the perpendicular split in
+    float32 (compute_perpendicular_component :80-104), the recombination in
+    float64, cast back at the end.  Row-local over the channel axis.  The
+    reference's ``[N·T,1] × [N,T,C]`` broadcast only works for N = 1; this
+    restatement keeps that exact op order (tests use N = 1)."""
+    n, t, c = cond.shape
+    sigma = sigma.reshape(1, 1, 1).expand(n, 1, 1) if sigma.numel() == 1 else sigma.view(n, 1, 1)
+    w = guidance_scale - 1
+    w = w * (w > 0) + 1e-3
+    ht = latents - sigma * cond
+    hu = latents - sigma * uncond
+    diff = ht - hu
+    a, b = ht.view(-1, c).to(torch.float64), hu.reshape(-1, c).contiguous().to(torch.float64)
+    a = a / torch.linalg.norm(a, dim=1, keepdim=True)
+    b = b / torch.linalg.norm(b, dim=1, keepdim=True)
+    theta = torch.acos(torch.sum(a * b, dim=1, keepdim=True))
+    theta_new = torch.clip(w * theta, -angle_clip, angle_clip)
+    d32, u32 = diff.view(n * t, c).float(), hu.view(n * t, c).float()
+    dot = torch.sum(d32 * u32, dim=1, keepdim=True)
+    nsq = torch.sum(u32 * u32, dim=1, keepdim=True)
+    perp = (d32 - (dot / (nsq + 1e-8)) * u32).reshape(n, t, c)
+    if n == 1:
+        cs, sn, st = torch.cos(theta_new), torch.sin(theta_new), torch.sin(theta)
+    else:   # per-row generalisation (the reference raises a broadcast error here)
+        cs, sn, st = (v.view(n, t, 1) for v in (torch.cos(theta_new), torch.sin(theta_new), torch.sin(theta)))
+    v_new = cs * ht
+    p_new = perp * sn / st * (st > 1e-3) + perp * w * (st <= 1e-3)
+    new = v_new + p_new
+    return ((latents - new) / sigma).reshape(n, t, c).to(latents.dtype)
+
+
 def generate_base(forward: Callable[[Tensor, Tensor], Tensor], noise: Tensor,
                   infer_steps: int, guidance: float = 7.0, shift: float = 1.0,
                   infer_method: str = "ode", cfg_interval_start: float = 0.0,
                   cfg_interval_end: float = 1.0, timesteps: Optional[Tensor] = None,
-                  step_hook=None) -> Tensor:
+                  step_hook=None, use_adg: bool = False) -> Tensor:
     """The base/sft step loop (base:1864-1979) with ``forward(x, t_vec)``
     standing in for the decoder call (the batch is doubled for CFG by this
-    function, exactly as base:1929).  APG only (use_adg=False)."""
+    function, exactly as base:1929).  APG, or ADG with ``use_adg`` (base:1949-1964)."""
     dtype, device = noise.dtype, noise.device
     t = base_schedule(infer_steps, shift, dtype, device, timesteps)
     n_steps = len(t) - 1
@@ -115,7 +150,8 @@ def generate_base(forward: Callable[[Tensor, Tensor], Tensor], noise: Tensor,
         if do_cfg:
             cond, uncond = vt.chunk(2)
             if tc >= cfg_interval_start and tc <= cfg_interval_end:
-                vt = apg(cond, uncond, guidance, mom, dims=(1,))
+                vt = (adg(xt, cond, uncond, tc, guidance) if use_adg
+                      else apg(cond, uncond, guidance, mom, dims=(1,)))
             else:
                 vt = cond
         if step_hook is not None:

@@ -58,7 +58,7 @@ def test_bf16_t_scale_rounding():
 
 
 SAMPLERS = ["base_s8_sh3", "base_s27_sh3", "base_s60_sh3", "base_s10_sh1_interval",
-            "base_s8_nocfg_fp32", "turbo_sh3", "turbo_sh2", "turbo_custom"]
+            "base_s8_nocfg_fp32", "base_s8_adg", "turbo_sh3", "turbo_sh2", "turbo_custom"]
 
 
 def _replay(g):
@@ -85,7 +85,7 @@ def test_sampler_bit_exact(name):
         out = sampler_oracle.generate_base(
             fwd, noise, kw["infer_steps"], guidance=kw["diffusion_guidance_sale"],
             shift=kw.get("shift", 1.0), cfg_interval_start=kw.get("cfg_interval_start", 0.0),
-            cfg_interval_end=kw.get("cfg_interval_end", 1.0))
+            cfg_interval_end=kw.get("cfg_interval_end", 1.0), use_adg=kw.get("use_adg", False))
     else:
         ts = None
         if "timesteps" in kw:
@@ -94,6 +94,18 @@ def test_sampler_bit_exact(name):
         out = sampler_oracle.generate_turbo(fwd, noise, shift=kw.get("shift", 3.0), timesteps=ts)
     assert st["i"] == meta["n_calls"]
     assert torch.equal(out, g["target_latents"])
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_adg_direct_bit_exact(i):
+    """adg_forward on seeded inputs, incl. a near-parallel row whose fp64 cos
+    rounds above 1 (acos → NaN in the reference for some sigmas)."""
+    g = load_golden("adg_direct")
+    guidance = golden_manifest()["adg"]["direct"]["guidance"]
+    out = sampler_oracle.adg(g[f"x_{i}"], g[f"cond_{i}"], g[f"uncond_{i}"], g[f"sigma_{i}"], guidance)
+    ref = g[f"out_{i}"]
+    assert torch.equal(out.isnan(), ref.isnan())
+    assert torch.equal(torch.nan_to_num(out), torch.nan_to_num(ref))
 
 
 def test_noise_matches_reference_generator():

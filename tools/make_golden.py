@@ -11,7 +11,8 @@ Fixtures:
   dit_fwd_*.safetensors      one decoder forward (tiny + full-width configs,
                              fp32 + bf16, even/odd T)
   temb_*.safetensors         TimestepEmbedding outputs for schedule values
-  sampler_*.safetensors      a whole generate_audio (base CFG+APG / turbo)
+  adg_*.safetensors          adg_forward on seeded inputs (ADG guidance)
+  sampler_*.safetensors      a whole generate_audio (base CFG+APG or ADG / turbo)
                              driven by a deterministic stand-in decoder that
                              records every (x, t, vt) — pins schedules, APG,
                              momentum, Euler/x0 arithmetic bit-exactly.
@@ -179,6 +180,45 @@ def gen_sampler(variant, name, dtype, B, T, **gen_kw):
             "kwargs": meta}
 
 
+def gen_adg_direct(name, B, T, seed, sigmas, guidance):
+    """adg_forward (apg_guidance.py:107-180) called directly on seeded bf16
+    inputs — includes rows where cond == uncond (θ = 0 branch) and a fully
+    aligned row pair (sin θ ≤ 1e-3 branch)."""
+    _import_ref("base")
+    import apg_guidance as ag
+    g = torch.Generator().manual_seed(seed)
+    tensors = {}
+    for i, sg in enumerate(sigmas):
+        x = torch.randn(B, T, 64, generator=g).bfloat16()
+        c = torch.randn(B, T, 64, generator=g).bfloat16()
+        u = (c.float() + 0.3 * torch.randn(B, T, 64, generator=g)).bfloat16()
+        u[:, 3] = (c[:, 3].float() * 1.0005).bfloat16()      # nearly parallel hats
+        s = torch.tensor(sg, dtype=torch.bfloat16)
+        out = ag.adg_forward(latents=x, noise_pred_cond=c, noise_pred_uncond=u, sigma=s,
+                             guidance_scale=guidance)
+        tensors.update({f"x_{i}": x, f"cond_{i}": c, f"uncond_{i}": u, f"sigma_{i}": s.reshape(1),
+                        f"out_{i}": out.contiguous()})
+    save_file(tensors, os.path.join(OUT, f"adg_{name}.safetensors"))
+    return {"B": B, "T": T, "sigmas": sigmas, "guidance": guidance}
+
+
+def main_only(which):
+    """Add fixtures to an existing manifest without regenerating the rest."""
+    torch.set_num_threads(8)
+    mpath = os.path.join(OUT, "manifest.json")
+    manifest = json.load(open(mpath))
+    bf = torch.bfloat16
+    if "adg" in which:
+        manifest["adg"] = {"direct": gen_adg_direct("direct", 1, 48, 5, [1.0, 0.75, 0.30078125, 0.05],
+                                                    7.0)}
+        manifest["sampler"]["base_s8_adg"] = gen_sampler("base", "base_s8_adg", bf, 1, 40, infer_steps=8,
+                                                         shift=3.0, diffusion_guidance_sale=7.0,
+                                                         use_adg=True)
+    with open(mpath, "w") as f:
+        json.dump(manifest, f, indent=1, default=str)
+    print("updated", mpath)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
@@ -226,4 +266,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        main_only(sys.argv[2].split(","))
+    else:
+        main()

@@ -6,7 +6,7 @@ FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so it
 is doubled; WRITE_SIZE is exact for 16-B stores.  Kernels are keyed by
 template instance + grid (each GEMM shape its own row).
 
-usage: pmc_traffic.py FETCH_DB WRITE_DB [OUT_JSON]
+usage: pmc_traffic.py FETCH_DB WRITE_DB [OUT_JSON [M]]
 """
 import json
 import re
@@ -49,12 +49,11 @@ if __name__ == "__main__":
     for k, v in sorted(t.items(), key=lambda kv: -kv[1]["hbm_bytes"])[:30]:
         print(f"{k[:100]:100s} {v['hbm_bytes'] / 1e6:10.2f} MB  (fetch {v['fetch_bytes'] / 1e6:.2f}, write {v['write_bytes'] / 1e6:.2f})")
     if len(sys.argv) > 3:
-        sw = [v for k, v in t.items() if k.startswith("gemm_kernel") and k.endswith(", 3>" + k.split(", 3>")[-1])
-              and "EPI" not in k]
-        sw = [v for k, v in t.items() if re.match(r"gemm_kernel<.*, 3> grid=", k)]
+        sw = [v for k, v in t.items() if re.match(r"gemm(_pp)?_kernel<.*, 3> grid=", k)]
         doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace on tools/prof_dit.py "
                          "(separate passes; FETCH x2 gfx950 correction; KB -> bytes)",
                "kernels": t}
         if sw:
             doc["gemm_swiglu_hbm_bytes_per_launch"] = max(v["hbm_bytes"] for v in sw)
+            doc["gemm_swiglu_M"] = int(sys.argv[4]) if len(sys.argv) > 4 else 6000   # Bc·S of the profiled run
         json.dump(doc, open(sys.argv[3], "w"), indent=1)
