@@ -13,9 +13,11 @@
 // head_post), o token-major [B][Sq][o_ld] at column h·128.
 //
 // Structure: workgroup = the NREP query heads of one KV head (GQA sharing)
-// × 4 waves × 32 queries; KV tiles of 64 keys, double-buffered in LDS with
-// the next tile's global loads in flight during the current tile's MFMAs
-// (register prefetch, written after the MFMAs, one barrier per tile), staged (rows of 256 B, 16-B chunks XOR-swizzled so that the
+// × 4 waves × 32 queries; KV tiles of 64 keys in a 3-deep LDS ring, the next
+// tile's LDS-DMA (global_load_lds, swizzle applied on the source) in flight
+// during the current tile's MFMAs, one barrier per tile; the
+// second head's waves run P·V one tile late so SIMD partners alternate
+// softmax and MFMA work; tiles are stored as rows of 256 B, 16-B chunks XOR-swizzled so that the
 // K row reads (ds_read_b128) and the V transposed reads (ds_read_b64_tr_b16)
 // are bank-conflict free).  Per wave, v_mfma_f32_32x32x16_bf16 computes the
 // swapped score tile Sᵀ = K·Qᵀ, so each lane owns one query row: the row
@@ -28,6 +30,13 @@
 
 namespace acehip {
 namespace {
+
+#ifndef ATT_DEFER
+#define ATT_DEFER 0        // second head's waves run P·V one tile late (SIMD-partner stagger;
+#endif                     // measured neutral-to-negative on MI355X, kept as an A/B switch)
+#ifndef ATT_PRIO
+#define ATT_PRIO 1         // static s_setprio 1 for the deferred (younger) half
+#endif
 
 constexpr int QB = 128;    // queries per workgroup
 constexpr int KT = 64;     // keys per tile
@@ -49,8 +58,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   int64_t o_ld) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
-    constexpr int CH = 2 * KT * 16 / NT;           // 16-B chunks per thread per tile (K and V)
-    __shared__ __attribute__((aligned(16))) char lds[2 * 2 * TILE];   // [buf][K|V]
+    constexpr int NBUF = ATT_DEFER ? 3 : 2;        // K/V ring (deferred P·V still reads V(j−1))
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
     const int b = blockIdx.z, kvh = blockIdx.y;
@@ -58,6 +67,12 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const int qblk = blockIdx.x * QB;
     const int q0 = qblk + (wave & 3) * 32;
     const int qi = q0 + r;
+    // SIMD partners (wave w and w+4) are staggered: the second half defers each
+    // tile's P·V into the next iteration, so one partner's softmax (VALU) runs
+    // beside the other's MFMAs; the younger half gets static priority
+    // (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
+    const bool defer = ATT_DEFER && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4;
+    if (ATT_PRIO && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[qi][16s + 8hh .. +8]
     const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi, Sq - 1)) * 128;
@@ -72,27 +87,24 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         kv_lo = max(0, qblk - window);
         kv_hi = min(Sk, qblk + QB + window);
     }
+    const int wlim = window >= 0 ? window : 0x7fffffff;
     const int t_first = kv_lo / KT;
     const int ntiles = (kv_hi + KT - 1) / KT - t_first;
 
-    // register prefetch of one K/V tile: chunk c → (K|V, row, 16-B column chunk)
-    uint4 pre[CH];
-    auto load_tile = [&](int kv0) {
+    // LDS-DMA staging of one K/V tile (32 KiB = 32 wave-instructions of 1 KiB, 4 per
+    // wave): instruction c covers image rows 4c..4c+3 of K (c < 16) or V; lane L
+    // writes the 16-B slot (row 4c + L/16, physical chunk L%16), so it fetches the
+    // logical chunk that kvoff() places there (the XOR is an involution).  Rows
+    // past Sk are clamped to a real row: those keys are masked (K) or meet P = 0 (V).
+    auto stage_tile = [&](int kv0, int buf) {
+        char *base = lds + buf * 2 * TILE;
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const int c = tid + NT * i;                // 0 .. 2·64·16
-            const int isv = c >> 10, rc = c & 1023;
-            const int row = rc >> 4, ch = rc & 15, key = kv0 + row;
-            pre[i] = make_uint4(0, 0, 0, 0);
-            if (key < Sk) pre[i] = *(const uint4 *)((isv ? vp : kp) + (int64_t)key * 128 + ch * 8);
-        }
-    };
-    auto store_tile = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const int c = tid + NT * i;
-            const int isv = c >> 10, rc = c & 1023;
-            *(uint4 *)(lds + buf * 2 * TILE + isv * TILE + kvoff(rc >> 4, rc & 15)) = pre[i];
+        for (int i = 0; i < 32 / (NT / 64); ++i) {
+            const int c = wave * (32 / (NT / 64)) + i;
+            const int isv = c >> 4, row = (c & 15) * 4 + (lane >> 4), pc = lane & 15;
+            const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+            const int key = min(kv0 + row, Sk - 1);
+            glds16((isv ? vp : kp) + (int64_t)key * 128 + ch * 8, base + isv * TILE + (c & 15) * 1024);
         }
     };
 
@@ -103,86 +115,9 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
 #pragma unroll
         for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
 
-    load_tile(t_first * KT);
-    store_tile(0);
-    __syncthreads();
     const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
-    for (int it = 0; it < ntiles; ++it) {
-        const int kv0 = (t_first + it) * KT;
-        const int cur = it & 1;
-        const bool more = it + 1 < ntiles;
-        if (more) load_tile(kv0 + KT);           // in flight during this tile's MFMAs
-        const char *ldsK = lds + cur * 2 * TILE;
-        const char *ldsV = ldsK + TILE;
-
-        // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
-        f32x16 st[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const bf16x8 kf = *(const bf16x8 *)(ldsK + kvoff(32 * t + r, 2 * s + hh));
-                st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
-            }
-        }
-        // scale (log2 domain) + mask + running max; interior tiles of full /
-        // cross attention need no mask
-        float mx = NEG;
-        if (window < 0 && kv0 + KT <= Sk) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    st[t][j] *= sl2;
-                    mx = fmaxf(mx, st[t][j]);
-                }
-        } else {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
-                    bool ok = kj < Sk;
-                    if (window >= 0) ok = ok && abs(qi - kj) <= window;
-                    const float sv = ok ? st[t][j] * sl2 : NEG;
-                    st[t][j] = sv;
-                    mx = fmaxf(mx, sv);
-                }
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(m, mx);
-        const float alpha = exp2f(m - mn);
-        m = mn;
-        float rs = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const float p = exp2f(st[t][j] - mn);
-                st[t][j] = p;
-                rs += p;
-            }
-        rs += __shfl_xor(rs, 32, 64);
-        l = l * alpha + rs;
-        if (__any(alpha != 1.0f)) {                  // skip the O rescale when no row's max grew
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
-        }
-
-        // P (bf16) as the B operand: tile t, k-step s ← registers 8s..8s+7
-        bf16x8 pf[2][2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
-
-        // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads
+    // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads
+    auto pv = [&](const char *ldsV, const bf16x8 (&pf)[2][2]) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             const int dc = 32 * dt + 16 * (g & 1);
@@ -203,9 +138,99 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                     oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
                 }
         }
-        if (more) store_tile(cur ^ 1);             // tile it-1's buffer: every wave left it before the last barrier
+    };
+
+    stage_tile(t_first * KT, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
+    for (int it = 0; it < ntiles; ++it) {
+        const int kv0 = (t_first + it) * KT;
+        const int cur = it % NBUF;
+        const bool more = it + 1 < ntiles;
+        if (more) stage_tile(kv0 + KT, (it + 1) % NBUF);   // tile it−2's slot: read by nobody now
+        const char *ldsK = lds + cur * 2 * TILE;
+        const char *ldsV = ldsK + TILE;
+        // deferred half: the previous tile's P·V first (O is still at that tile's max)
+        if (defer && it > 0) pv(lds + ((it + NBUF - 1) % NBUF) * 2 * TILE + TILE, pf);
+        // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
+        // skipped (the wave still joins the barrier); one entirely inside needs no mask
+        const bool outside = window >= 0 && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window);
+        const bool interior = kv0 + KT <= Sk &&
+                              (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window));
+        if (outside && !defer) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            continue;
+        }
+
+        // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
+        f32x16 st[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 kf = *(const bf16x8 *)(ldsK + kvoff(32 * t + r, 2 * s + hh));
+                st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
+            }
+        }
+        // running max on raw scores (scale folded into the exp2 FMA below);
+        // interior tiles of full / cross attention need no mask
+        float mx = NEG;
+        if (interior) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) mx = fmaxf(mx, st[t][j]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
+                    // branch-free: window < 0 ⇒ wlim = INT_MAX
+                    const bool ok = (kj < Sk) & (abs(qi - kj) <= wlim);
+                    const float sv = ok ? st[t][j] : NEG;
+                    st[t][j] = sv;
+                    mx = fmaxf(mx, sv);
+                }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+        const float mn = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);   // raw v_exp_f32 (no denormal range fix-up)
+        m = mn;
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(st[t][j], sl2, -mn));
+                st[t][j] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        if (__any(alpha != 1.0f)) {                  // skip the O rescale when no row's max grew
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) oacc[i][j] *= alpha;
+        }
+
+        // P (bf16) as the B operand: tile t, k-step s ← registers 8s..8s+7
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
+        if (!defer) pv(ldsV, pf);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own DMA landed; the barrier publishes it
         __syncthreads();
     }
+    if (defer && ntiles > 0) pv(lds + ((ntiles - 1) % NBUF) * 2 * TILE + TILE, pf);
 
     if (qi >= Sq) return;
     const float inv = 1.0f / l;

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     constexpr int NINS = ROWS / 8;                     // glds instructions per stage
     constexpr int PER_WAVE = NINS / NW;
     static_assert(NINS % NW == 0, "staging must split evenly over waves");
-    static_assert(EPI != EPI_SWIGLU || TN == 64, "SwiGLU pairs 32+32 columns per wave");
+    static_assert(EPI != EPI_SWIGLU || TN % 64 == 0, "SwiGLU pairs 32+32 columns per 64-column panel");
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -124,19 +124,21 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
         const int m = m0 + wm * TM + i * 16 + fr;
         if (m >= a.M) continue;
         if constexpr (EPI == EPI_SWIGLU) {
-            // packed rows: within each 64-row wave panel, rows [0,32) gate, [32,64) up
+            // packed rows: within each 64-row panel, rows [0,32) gate, [32,64) up
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int nout = ((n0 + wn * 64) >> 1) + j * 16 + fc * 4;
-                float o[4];
+            for (int pnl = 0; pnl < TN / 64; ++pnl)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float g = rbf(acc[i][j][r]);
-                    const float u = rbf(acc[i][j + 2][r]);
-                    o[r] = rbf(silu_f(g)) * u;
+                for (int j = 0; j < 2; ++j) {
+                    const int nout = ((n0 + wn * TN + pnl * 64) >> 1) + j * 16 + fc * 4;
+                    float o[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float g = rbf(acc[i][4 * pnl + j][r]);
+                        const float u = rbf(acc[i][4 * pnl + j + 2][r]);
+                        o[r] = rbf(silu_f(g)) * u;
+                    }
+                    *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
                 }
-                *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
-            }
         } else {
             const int b = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
 #pragma unroll
@@ -407,6 +409,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 6: return launch<192, 256, 2, 4, 2>(a, s);   // 8 waves, 96x64 wave tile (112 KiB)
         case 7: return launch_pp<256>(a, s);              // ping-pong 256x256 (128 KiB)
         case 8: return launch_pp<192>(a, s);              // ping-pong 192x256 (112 KiB)
+        case 9: return launch<192, 256, 2, 2, 2>(a, s);   // 4 waves (1/SIMD), 96x128 wave tile, acc in AGPRs
+        case 10: return launch<256, 256, 2, 2, 2>(a, s);  // 4 waves (1/SIMD), 128x128 wave tile
         default: return fail(-1, "gemm: bad variant");
     }
 }

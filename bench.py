@@ -203,7 +203,7 @@ def main():
         "dit_tflops": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
         "dit_mfma_frac": round(dit_flops_song / (dit_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
         "vae_tflops": round(vae_flops_song / (vae_ms * 1e-3) / 1e12, 1) if vae is not None else None,
-        "roofline": {"bound": "mfma", "kernel": "gemm_kernel<EPI_SWIGLU> (M=%d N=%d K=%d)" % (
+        "roofline": {"bound": "mfma", "kernel": "SwiGLU gate/up GEMM, EPI_SWIGLU (M=%d N=%d K=%d)" % (
             M, 2 * cfg.intermediate_size, cfg.hidden_size),
             "achieved": round(sw_tflops, 1) if sw_tflops else None, "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": round(sw_tflops / PEAK_BF16_TFLOPS, 4) if sw_tflops else None,

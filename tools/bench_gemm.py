@@ -10,6 +10,12 @@ dev = torch.device("cuda:0")
 shapes = {"swiglu": (6000, 12288, 2048), "down": (6000, 2048, 6144), "qkv": (6000, 4096, 2048),
           "o": (6000, 2048, 2048), "vae_k7_c128": (46080, 128, 896), "vae_k7_c512": (360000 // 4, 512, 3584)}
 variants = [int(v) for v in os.environ.get("VARIANTS", "0,4,6,7,8").split(",")]
+# COLD=1: rotate through enough weight copies (> 512 MB) that W comes from HBM
+# every launch, as in the DiT forward (1.2 GB of weights per step, MALL 256 MB)
+COLD = os.environ.get("COLD", "0") == "1"
+only = os.environ.get("SHAPES")
+if only:
+    shapes = {k: v for k, v in shapes.items() if k in only.split(",")}
 res = {}
 for name, (M, N, K) in shapes.items():
     g = torch.Generator(device=dev).manual_seed(0)
@@ -17,14 +23,20 @@ for name, (M, N, K) in shapes.items():
     W = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.05).bfloat16()
     ref = (A.float() @ W.float().t())
     C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    nrot = max(1, int(600e6 // (N * K * 2))) if COLD else 1
+    Ws = [W] + [W.clone() for _ in range(nrot - 1)]
+    rot = [0]
     fl = 2.0 * M * N * K
     row = {}
     for v in variants:
-        if v in (3, 5, 6, 7, 8) and N % 256:
+        if v in (3, 5, 6, 7, 8, 9, 10) and N % 256:
             continue
         def run():
-            ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, None, 0, v,
+            Wr = Ws[rot[0] % nrot]
+            rot[0] += 1
+            ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(Wr), K, ff.ptr(C), N, M, N, K, None, 0, v,
                                                   ff.stream_ptr()))
+        rot[0] = 0
         run(); torch.cuda.synchronize()
         err = float((C.float() - ref).norm() / ref.norm())
         for _ in range(3): run()
@@ -35,11 +47,11 @@ for name, (M, N, K) in shapes.items():
         e1.record(); torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1e3
         row[f"v{v}"] = {"us": round(us, 1), "tflops": round(fl / us * 1e-6, 1), "rel": round(err, 5)}
-    Wt = W.t()
-    for _ in range(3): torch.matmul(A, Wt)
+    Wts = [w.t() for w in Ws]
+    for i in range(3): torch.matmul(A, Wts[i % nrot])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20): torch.matmul(A, Wt)
+    for i in range(20): torch.matmul(A, Wts[i % nrot])
     e1.record(); torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 20 * 1e3
     row["torch(hipBLASLt)"] = {"us": round(us, 1), "tflops": round(fl / us * 1e-6, 1)}
