@@ -126,7 +126,10 @@ class DiTRuntime:
     PROFILE_KINDS = ["gemm_swiglu", "gemm_down", "gemm_qkv", "gemm_o", "attn_full", "attn_band",
                      "attn_cross"]
 
-    def profile(self, enable: bool = True):
+    def profile(self, enable: bool = True, kinds=None):
+        """Record HIP events around the listed kernel families (default: all)."""
+        mask = 0x7f if kinds is None else sum(1 << self.PROFILE_KINDS.index(k) for k in kinds)
+        check(lib().acehip_dit_profile_kinds(self.h, mask), "dit_profile_kinds")
         check(lib().acehip_dit_profile(self.h, 1 if enable else 0), "dit_profile")
 
     def profile_read(self) -> Dict[str, tuple]:

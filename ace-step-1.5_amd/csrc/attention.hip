@@ -42,6 +42,14 @@ constexpr int QB = 128;    // queries per workgroup
 constexpr int KT = 64;     // keys per tile
 constexpr float NEG = -1e30f;
 
+// tail balancing: units [0, full) run whole; each later unit runs as nsplit
+// KV-range parts whose partial (O, m, l) meet in ws, merged by the last part
+struct SplitArgs {
+    int nq, full, nsplit;
+    float *ws;     // ≥ (units − full)·nsplit·8·66·64 floats
+    int *cnt;      // ≥ units − full ints, zero between launches
+};
+
 __device__ __forceinline__ int kvoff(int row, int ch) {
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
@@ -55,16 +63,25 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const bf16_t *__restrict__ v,
                                                                   bf16_t *__restrict__ o, int H, int KV,
                                                                   int Sq, int Sk, int window, float sl2,
-                                                                  int64_t o_ld) {
+                                                                  int64_t o_ld, SplitArgs sp) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
     constexpr int NBUF = ATT_DEFER ? 3 : 2;        // K/V ring (deferred P·V still reads V(j−1))
     __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
-    const int b = blockIdx.z, kvh = blockIdx.y;
+    // work unit u = (b, kvh, q-block), q-block fastest; blocks past sp.full are the
+    // KV-range parts of the tail units (tail balancing, see attention())
+    int u = blockIdx.x, part = 0, nsplit = 1;
+    if (u >= sp.full) {
+        const int j = u - sp.full;
+        u = sp.full + j / sp.nsplit;
+        part = j % sp.nsplit;
+        nsplit = sp.nsplit;
+    }
+    const int qb = u % sp.nq, kvh = (u / sp.nq) % KV, b = u / (sp.nq * KV);
     const int hq = kvh * NREP + (wave >> 2);
-    const int qblk = blockIdx.x * QB;
+    const int qblk = qb * QB;
     const int q0 = qblk + (wave & 3) * 32;
     const int qi = q0 + r;
     // SIMD partners (wave w and w+4) are staggered: the second half defers each
@@ -88,8 +105,14 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         kv_hi = min(Sk, qblk + QB + window);
     }
     const int wlim = window >= 0 ? window : 0x7fffffff;
-    const int t_first = kv_lo / KT;
-    const int ntiles = (kv_hi + KT - 1) / KT - t_first;
+    int t_first = kv_lo / KT;
+    int ntiles = (kv_hi + KT - 1) / KT - t_first;
+    if (nsplit > 1) {                              // this part's contiguous tile range
+        const int per = (ntiles + nsplit - 1) / nsplit;
+        const int t0 = min(ntiles, part * per), t1 = min(ntiles, t0 + per);
+        t_first += t0;
+        ntiles = t1 - t0;
+    }
 
     // LDS-DMA staging of one K/V tile (32 KiB = 32 wave-instructions of 1 KiB, 4 per
     // wave): instruction c covers image rows 4c..4c+3 of K (c < 16) or V; lane L
@@ -140,7 +163,7 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         }
     };
 
-    stage_tile(t_first * KT, 0);
+    if (ntiles > 0) stage_tile(t_first * KT, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
@@ -232,6 +255,44 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     }
     if (defer && ntiles > 0) pv(lds + ((ntiles - 1) % NBUF) * 2 * TILE + TILE, pf);
 
+    if (nsplit > 1) {
+        // publish this part's (O, m, l) in lane order, then take a ticket; the last
+        // part merges the others (they published before their tickets) — no spinning.
+        // Agent-scope relaxed atomic stores/loads (sc1: coherent across the XCDs' L2s)
+        // plus vmcnt(0) order the hand-off; a __threadfence() would write back and
+        // invalidate the whole L2 and evict every co-resident workgroup's K/V tiles.
+        const int64_t wsz = 66 * 64;                   // floats per wave: 64 O + m + l per lane
+        float *mine = sp.ws + (((int64_t)(u - sp.full) * nsplit + part) * 8 + wave) * wsz;
+        auto st_c = [](float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        auto ld_c = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) st_c(mine + (16 * i + j) * 64 + lane, oacc[i][j]);
+        st_c(mine + 64 * 64 + lane, m);
+        st_c(mine + 65 * 64 + lane, l);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ int s_ticket;
+        if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
+        __syncthreads();
+        if (s_ticket != nsplit - 1) return;
+        for (int p2 = 0; p2 < nsplit; ++p2) {
+            if (p2 == part) continue;
+            const float *oth = sp.ws + (((int64_t)(u - sp.full) * nsplit + p2) * 8 + wave) * wsz;
+            const float m2 = ld_c(oth + 64 * 64 + lane), l2 = ld_c(oth + 65 * 64 + lane);
+            const float mn = fmaxf(m, m2);
+            const float a1 = __builtin_amdgcn_exp2f(m - mn), a2 = __builtin_amdgcn_exp2f(m2 - mn);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) oacc[i][j] = oacc[i][j] * a1 + ld_c(oth + (16 * i + j) * 64 + lane) * a2;
+            l = l * a1 + l2 * a2;
+            m = mn;
+        }
+        if (tid == 0) sp.cnt[u - sp.full] = 0;         // self-resetting for the next launch
+    }
+
     if (qi >= Sq) return;
     const float inv = 1.0f / l;
     bf16_t *op = o + ((int64_t)b * Sq + qi) * o_ld + hq * 128;
@@ -249,19 +310,57 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
 
 }  // namespace
 
+static int num_cus_attn() {
+    // ACEHIP_ATTN_CUS overrides the CU count the tail split plans for (tests use it
+    // to exercise 3- and 4-way splits on small shapes)
+    if (const char *e = getenv("ACEHIP_ATTN_CUS")) {
+        const int v = atoi(e);
+        if (v > 0) return v;
+    }
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+size_t attention_ws_bytes() {
+    const size_t cus = std::max<size_t>(1024, (size_t)num_cus_attn());
+    return cus * 8 * 66 * 64 * sizeof(float) + cus * sizeof(int);   // ≤ cus split parts in flight
+}
+
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
-              int Sq, int Sk, int window, float scale, int64_t o_ld, hipStream_t s) {
+              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s) {
     if (B <= 0 || Sq <= 0) return 0;
     if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
     if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
     const int nrep = H / KV;
     const float sl2 = scale * 1.4426950408889634f;
+    const int nq = (Sq + QB - 1) / QB;
+    const int units = nq * KV * B;
+    SplitArgs sp{nq, units, 1, nullptr, nullptr};
+    // one workgroup per CU: a partial last round of whole units is replaced by
+    // tail units split over ⌊CUs / tail⌋ KV ranges (1.5 rounds instead of 2 at
+    // 384 units on 256 CUs)
+    const int cus = num_cus_attn();
+    const int tail = units % cus;
+    // only long KV loops pay for the partial write + merge (measured: full attention
+    // at S = 3000, 47 tiles, −27 %; band (≈7 tiles) and cross (11 tiles) lose)
+    const int unit_tiles = window >= 0 ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
+    if (ws && nrep == 2 && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
+        sp.full = units - tail;
+        sp.nsplit = min(4, cus / tail);
+        sp.cnt = (int *)ws;
+        sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
+    }
+    const int grid = sp.full + (units - sp.full) * sp.nsplit;
     if (nrep == 2) {
-        dim3 grid((Sq + QB - 1) / QB, KV, B);
-        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld);
+        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
     } else if (nrep == 1) {
-        dim3 grid((Sq + QB - 1) / QB, KV, B);
-        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld);
+        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
     } else {
         return fail(-1, "attention: heads/kv_heads must be 1 or 2");
     }

@@ -60,6 +60,7 @@ struct acehip_dit {
     float *freqs = nullptr;          // [128] sinusoid frequencies
     float *inv_freq_host = nullptr;  // optional override, [hd/2]
     std::vector<float> inv_freq_override;
+    bf16_t *attn_ws = nullptr;  // attention tail-split workspace (attention_ws_bytes())
     bf16_t *rope_cos = nullptr, *rope_sin = nullptr;   // [max_S][hd]
 
     // workspace
@@ -72,6 +73,7 @@ struct acehip_dit {
     // optional per-kernel event timing (acehip_dit_profile)
     static constexpr int NKIND = 7, NPAIR = 16384;
     bool prof = false;
+    unsigned prof_mask = 0x7f;         // kinds recorded while profiling (acehip_dit_profile_kinds)
     std::vector<hipEvent_t> ev;        // 2·NPAIR events
     std::vector<int> ev_kind;          // kind of each recorded pair
     int ev_used = 0;
@@ -130,7 +132,7 @@ int build_rope(acehip_dit *h) {
 // record an event pair around `launch` when profiling is on
 template <class F>
 int timed(acehip_dit *h, int kind, hipStream_t s, F &&launch) {
-    if (!h->prof || h->ev_used >= acehip_dit::NPAIR) return launch();
+    if (!h->prof || !((h->prof_mask >> kind) & 1u) || h->ev_used >= acehip_dit::NPAIR) return launch();
     const int i = h->ev_used++;
     h->ev_kind[i] = kind;
     HIP_TRY(hipEventRecord(h->ev[2 * i], s));
@@ -249,6 +251,11 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
     h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
     h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
+    {   // attention tail-split partials + self-resetting counters (zeroed once)
+        const size_t wb = attention_ws_bytes();
+        h->attn_ws = A((wb + 1) / 2);
+        if (h->attn_ws && hipMemset(h->attn_ws, 0, wb) != hipSuccess) ok = false;
+    }
     void *fr = nullptr;
     if (ok && hipMalloc(&fr, 128 * sizeof(float)) == hipSuccess) {
         h->allocs.push_back(fr);
@@ -478,7 +485,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         RUN(head_post(hp, s));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
             return attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
-                             scale, qd, s);
+                             scale, qd, h->attn_ws, s);
         }));
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
@@ -496,7 +503,8 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         cp.q = h->Qh; cp.S_dst = S; cp.eps = eps;
         RUN(head_post(cp, s));
         RUN(timed(h, 6, s, [&] {
-            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd, s);
+            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd,
+                             h->attn_ws, s);
         }));
         GemmArgs co{};
         co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
@@ -536,6 +544,12 @@ int acehip_dit_profile(acehip_dit *h, int enable) {
     }
     h->prof = enable != 0;
     h->ev_used = 0;
+    return 0;
+}
+
+int acehip_dit_profile_kinds(acehip_dit *h, unsigned mask) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    h->prof_mask = mask;
     return 0;
 }
 
@@ -610,8 +624,19 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
 
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,
                           int Sq, int Sk, int window, float scale, void *stream) {
+    // standalone entry (tests / micro-bench): one lazily allocated tail-split workspace
+    // per device (the DiT runtime owns its own, allocated at create)
+    static std::map<int, void *> ws_by_dev;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    void *&ws = ws_by_dev[dev];
+    if (!ws) {
+        const size_t wb = attention_ws_bytes();
+        if (hipMalloc(&ws, wb) != hipSuccess) return fail(ACEHIP_E_OOM, "attention workspace");
+        HIP_TRY(hipMemset(ws, 0, wb));
+    }
     return attention((const bf16_t *)q, (const bf16_t *)k, (const bf16_t *)v, (bf16_t *)o, B, H, KV, Sq,
-                     Sk, window, scale, (int64_t)H * 128, (hipStream_t)stream);
+                     Sk, window, scale, (int64_t)H * 128, ws, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -65,8 +65,11 @@ struct HeadPostArgs {
 int head_post(const HeadPostArgs &a, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---
+// ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials
+// + self-resetting counters), or null to disable tail balancing
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
-              int Sq, int Sk, int window, float scale, int64_t o_ld, hipStream_t s);
+              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s);
+size_t attention_ws_bytes();
 
 // --------------------------------------------------------------- sampler ---
 int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,

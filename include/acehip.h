@@ -112,6 +112,9 @@ int acehip_dit_destroy(acehip_dit *h);
  *       4 full self-attention, 5 band self-attention, 6 cross-attention. */
 int acehip_dit_profile(acehip_dit *h, int enable);
 int acehip_dit_profile_read(acehip_dit *h, int kind, int *launches, float *total_ms);
+/* Restrict recording to the kinds whose bit is set (default 0x7f = all): the
+ * bench times only the roofline kernel inside its timed region. */
+int acehip_dit_profile_kinds(acehip_dit *h, unsigned mask);
 
 /* ------------------------------------------------------------ sampler ---- */
 
