@@ -26,6 +26,7 @@ EXPORTS = [
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
     "acehip_vae_encode", "acehip_vae_destroy",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
+    "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16",
 ]
 
 
@@ -76,6 +77,9 @@ def _declare(lib):
                                         c_int, P]),
         "acehip_attention_bf16": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                           c_float, P]),
+        "acehip_rmsnorm_bf16": (c_int, [P, P, P, P, c_int64, c_int, P, c_int, c_int, c_float, c_int, P]),
+        "acehip_gemm_headpost_bf16": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                              P, P, P, P, c_float, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):

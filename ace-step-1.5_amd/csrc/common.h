@@ -17,16 +17,30 @@ __host__ __device__ __forceinline__ float bf2f(bf16_t v) {
     x.u = ((uint32_t)v) << 16;
     return x.f;
 }
-// round-to-nearest-even; NaN preserved (quiet)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// fp32 → bf16, round-to-nearest-even (torch's rounding for every bf16 op
+// output).  On the device this is gfx950's v_cvt_pk_bf16_f32 (RNE, one
+// instruction for two values); the host keeps the integer formulation — the
+// two agree on every non-NaN input, NaN stays NaN (payload may differ).
 __host__ __device__ __forceinline__ bf16_t f2bf(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bit_cast(bf16_t, (__bf16)f);
+#else
     union { uint32_t u; float f; } x;
     x.f = f;
     if ((x.u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((x.u >> 16) | 0x40);
     uint32_t r = x.u + 0x7fffu + ((x.u >> 16) & 1u);
     return (bf16_t)(r >> 16);
+#endif
 }
 // round an fp32 value through bf16 (models one torch bf16 op's output rounding)
 __host__ __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+// two fp32 → packed bf16 pair (low half = a)
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 
@@ -40,14 +54,10 @@ __device__ __forceinline__ void unpack8(const uint4 &u, float *f) {
     }
 }
 __device__ __forceinline__ uint4 pack8(const float *f) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 __device__ __forceinline__ uint2 pack4(const float *f) {
-    return make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
-                      (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+    return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
 }
 __device__ __forceinline__ void unpack4(const uint2 &u, float *f) {
     f[0] = bf2f((bf16_t)(u.x & 0xffff)); f[1] = bf2f((bf16_t)(u.x >> 16));

@@ -64,7 +64,7 @@ struct acehip_dit {
     bf16_t *rope_cos = nullptr, *rope_sin = nullptr;   // [max_S][hd]
 
     // workspace
-    bf16_t *X, *XN, *QKV, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
+    bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
@@ -238,7 +238,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     }
     // workspace
     const size_t S = cfg->max_S, Bc = cfg->max_Bc, M = S * Bc, Le = cfg->max_Lenc;
-    h->X = A(M * D); h->XN = A(M * D); h->QKV = A(M * (qd + 2 * kvd));
+    h->X = A(M * D); h->XN = A(M * D);
     h->Qh = A(M * qd); h->Kh = A(M * kvd); h->Vh = A(M * kvd); h->AO = A(M * qd);
     h->Hb = A(M * F); h->Xin = A(M * 384); h->O2 = A(M * 128);
     for (int e = 0; e < 2; ++e) {
@@ -473,16 +473,14 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         const int64_t mbs = 6 * D;
         // --- self-attention with AdaLN-Zero (base:499-511)
         RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, M, D, eps, s));
+        // QKV projection with q/k RMSNorm + RoPE + head-major scatter fused in the epilogue
         GemmArgs q{};
-        q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D; q.C = h->QKV; q.ldc = qd + 2 * kvd;
-        q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_STORE;
+        q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D;
+        q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_HEADPOST;
+        q.hp.B = Bc; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
+        q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
+        q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
         RUN(timed(h, 2, s, [&] { return gemm(q, s); }));
-        HeadPostArgs hp{};
-        hp.src = h->QKV; hp.ld_src = qd + 2 * kvd; hp.B = Bc; hp.S = S;
-        hp.nq = H; hp.nk = KV; hp.nv = KV; hp.qw = ly.qn; hp.kw = ly.kn;
-        hp.cos = h->rope_cos; hp.sin = h->rope_sin;
-        hp.q = h->Qh; hp.k = h->Kh; hp.v = h->Vh; hp.S_dst = S; hp.eps = eps;
-        RUN(head_post(hp, s));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
             return attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
                              scale, qd, h->attn_ws, s);
@@ -495,13 +493,11 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         // --- cross-attention, plain residual (base:513-526)
         RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
         GemmArgs cq{};
-        cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D; cq.C = h->QKV; cq.ldc = qd;
-        cq.M = M; cq.N = qd; cq.K = D; cq.epi = EPI_STORE;
+        cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D;
+        cq.M = M; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
+        cq.hp.B = Bc; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
+        cq.hp.eps = eps;
         RUN(gemm(cq, s));
-        HeadPostArgs cp{};
-        cp.src = h->QKV; cp.ld_src = qd; cp.B = Bc; cp.S = S; cp.nq = H; cp.qw = ly.cqn;
-        cp.q = h->Qh; cp.S_dst = S; cp.eps = eps;
-        RUN(head_post(cp, s));
         RUN(timed(h, 6, s, [&] {
             return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd,
                              h->attn_ws, s);
@@ -620,6 +616,35 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
     else return fail(ACEHIP_E_ARG, "gemm_ex: epilogue");
     if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
     return gemm_variant(g, variant, (hipStream_t)stream);
+}
+
+int acehip_rmsnorm_bf16(const void *x, const void *w, const void *shift, const void *scale,
+                        int64_t mod_bstride, int rows_per_batch, void *out, int M, int D, float eps,
+                        int rows_per_wave, void *stream) {
+    if (!x || !w || !out) return fail(ACEHIP_E_ARG, "null argument");
+    if (rows_per_wave == 3 || rows_per_wave > 4 || (rows_per_wave < 0 && rows_per_wave != -2 && rows_per_wave != -4))
+        return fail(ACEHIP_E_ARG, "rows_per_wave");
+    rmsnorm_set_rows(rows_per_wave);
+    const int rc = rmsnorm_mod((const bf16_t *)x, (const bf16_t *)w, (const bf16_t *)shift, (const bf16_t *)scale,
+                               mod_bstride, rows_per_batch, (bf16_t *)out, M, D, eps, (hipStream_t)stream);
+    rmsnorm_set_rows(0);
+    return rc;
+}
+
+int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int B, int S, int nq, int nk,
+                              int nv, const void *qw, const void *kw, const void *cos, const void *sin,
+                              float eps, void *q, void *k, void *v, void *stream) {
+    if (!A || !W) return fail(ACEHIP_E_ARG, "null argument");
+    if ((nq && !q) || (nk && !k) || (nv && !v)) return fail(ACEHIP_E_ARG, "missing head output");
+    GemmArgs g{};
+    g.A = (const bf16_t *)A; g.lda = lda; g.W = (const bf16_t *)W; g.ldw = K;
+    g.M = B * S; g.N = (nq + nk + nv) * 128; g.K = K; g.epi = EPI_HEADPOST;
+    if (g.M <= 0 || K % 64 || K <= 0) return fail(ACEHIP_E_ARG, "gemm_headpost: shape");
+    g.hp.B = B; g.hp.S = S; g.hp.nq = nq; g.hp.nk = nk; g.hp.nv = nv;
+    g.hp.qw = (const bf16_t *)qw; g.hp.kw = (const bf16_t *)kw;
+    g.hp.cos = (const bf16_t *)cos; g.hp.sin = (const bf16_t *)sin;
+    g.hp.q = (bf16_t *)q; g.hp.k = (bf16_t *)k; g.hp.v = (bf16_t *)v; g.hp.S_dst = S; g.hp.eps = eps;
+    return gemm(g, (hipStream_t)stream);
 }
 
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,

@@ -25,6 +25,7 @@
 //     and 192×256, two wave groups one barrier apart so MFMA and LDS traffic
 //     overlap on every SIMD), picked per shape by gemm_pick_variant.
 #include "kernels.h"
+#include "headpost.h"
 
 namespace acehip {
 namespace {
@@ -317,6 +318,68 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
     if (wr == 0) bar();   // balance the barrier count
 
+    if constexpr (EPI == EPI_HEADPOST) {
+        // bf16(acc) → LDS tile [BM][PITCH] (the operand ring is dead), then one 16-lane group
+        // per (row, 128-column head): RMSNorm + RoPE + head-major store.  A lane's units are
+        // uu = wave·4 + 32·it + sub: a fixed head (hh = sub & 1) and rows
+        // r = wave·2 + (sub >> 1) + 16·it, so (batch, position) advance incrementally (no
+        // integer division per unit) and every cos/sin row is loaded BEFORE the first store
+        // (a load's vmcnt would otherwise also wait for the older stores).
+        constexpr int PITCH = 264;   // 528-B rows: 16-B aligned, 2-way conflicts on the 8-B writes
+        constexpr int ITER = BM * 2 / 32;
+        static_assert(BM * PITCH * 2 <= 2 * BUF, "head-post staging tile must fit the operand ring");
+        const HeadPostArgs &h = a.hp;
+        const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = sub & 1;
+        const int head = (n0 >> 7) + hh;
+        const bool norm = head < h.nq + h.nk;
+        const bool rope = h.cos != nullptr;
+        const int r0 = wave * 2 + (sub >> 1);
+        const int mf = min(m0 + r0, a.M - 1);
+        const int b0 = mf / h.S, s0 = mf - b0 * h.S;
+        uint4 cv[ITER], sv[ITER];
+        if (rope) {
+            int sq = s0;
+#pragma unroll
+            for (int it = 0; it < ITER; ++it) {
+                const int sc = min(sq, h.S - 1);
+                cv[it] = *(const uint4 *)(h.cos + (int64_t)sc * 128 + d);
+                sv[it] = *(const uint4 *)(h.sin + (int64_t)sc * 128 + d);
+                sq += 16;
+                while (sq >= h.S) sq -= h.S;
+            }
+        }
+        float w[8] = {};
+        if (norm) unpack8(*(const uint4 *)((head < h.nq ? h.qw : h.kw) + d), w);
+        bf16_t *st = (bf16_t *)lds;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < SM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                *(uint2 *)(st + (arow + i * 16 + fr) * PITCH + wc * 64 + j * 16 + fc * 4) = pack4(o);
+            }
+        __syncthreads();
+        int bq = b0, sq = s0;
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+            const int r = r0 + 16 * it;
+            float x[8], cs[8] = {}, sn[8] = {};
+            unpack8(*(const uint4 *)(st + r * PITCH + hh * 128 + d), x);
+            if (rope) {
+                unpack8(cv[it], cs);
+                unpack8(sv[it], sn);
+            }
+            const bf16_t *nw;
+            bf16_t *dst = head_dst(h, head, bq, sq, nw);
+            head_norm_rope(x, li, norm, w, rope, cs, sn, h.eps);
+            if (m0 + r < a.M && dst) *(uint4 *)(dst + d) = pack8(x);
+            sq += 16;
+            while (sq >= h.S) { sq -= h.S; ++bq; }
+        }
+        return;
+    }
+
     // epilogue: lane owns row m, columns n..n+3 of each 16x16 sub-tile
 #pragma unroll
     for (int i = 0; i < SM; ++i) {
@@ -374,6 +437,12 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_SWIGLU: gemm_pp_kernel<BM, EPI_SWIGLU><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_HEADPOST:
+            if constexpr (BM == 192) {
+                gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
+                break;
+            }
+            return fail(-1, "gemm: head-post epilogue needs the 192-row ping-pong tile");
         default: return fail(-1, "gemm: bad epilogue");
     }
     HIP_TRY(hipGetLastError());
@@ -390,7 +459,7 @@ int launch(const GemmArgs &a, hipStream_t s) {
         case EPI_GATED_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_GATED_RES><<<tiles, NT, 0, s>>>(a); break;
         case EPI_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_RES><<<tiles, NT, 0, s>>>(a); break;
         case EPI_SWIGLU: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_SWIGLU><<<tiles, NT, 0, s>>>(a); break;
-        default: return fail(-1, "gemm: bad epilogue");
+        default: return fail(-1, "gemm: bad epilogue for this variant");
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -451,6 +520,13 @@ int gemm(const GemmArgs &a, hipStream_t s) {
     if ((a.lda | a.ldw | a.ldc) % 8) return fail(-1, "gemm: leading dims must be multiples of 8");
     if (a.epi == EPI_GATED_RES && (!a.gate || a.rows_per_batch <= 0)) return fail(-1, "gemm: gate");
     if ((a.epi == EPI_GATED_RES || a.epi == EPI_RES) && !a.res) return fail(-1, "gemm: res");
+    if (a.epi == EPI_HEADPOST) {
+        const HeadPostArgs &h = a.hp;
+        if (a.N % 256 || h.S <= 0 || (int64_t)h.B * h.S != a.M || (h.nq + h.nk + h.nv) * 128 != a.N ||
+            h.S_dst < h.S || (h.nq && !h.qw) || (h.nk && !h.kw) || (h.cos == nullptr) != (h.sin == nullptr))
+            return fail(-1, "gemm: head-post arguments inconsistent with the GEMM shape");
+        return launch_pp<192>(a, s);   // the fused epilogue exists for the 192-row tile only
+    }
     int v = g_variant_override;
     if (v < 0) v = gemm_pick_variant(a.M, a.N);
     if ((v == 3 || v >= 5) && a.N % 256) v = 0;

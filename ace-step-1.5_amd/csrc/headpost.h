@@ -1,0 +1,57 @@
+// headpost.h — the per-head q/k RMSNorm + RoPE transform shared by the
+// standalone head_post kernel (norm.hip) and the fused QKV / cross-Q GEMM
+// epilogue (gemm.hip, EPI_HEADPOST), so both paths round identically.
+//
+// Reference: q = q_norm(q_proj(x).view(.., 128)), k = k_norm(...) (base:304,338),
+// Qwen3RMSNorm (transformers modeling_qwen3.py:59-64: w · bf16(x·rsqrt(mean x²+eps))),
+// then rotate-half RoPE q·cos + rot(q)·sin with each product rounded to bf16
+// (modeling_qwen3.py:166-170).
+#pragma once
+#include "kernels.h"
+
+namespace acehip {
+
+// One 128-wide head is held by 16 consecutive lanes, 8 elements each
+// (d = 8·li, li = lane & 15).  Every lane of the wave must call this (it
+// shuffles); norm == false leaves x unchanged (v heads).  `rope` must be
+// uniform over the wave; w is this lane's 8 norm weights, cs/sn its 8 cos/sin.
+__device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm, const float (&w)[8], bool rope,
+                                               const float (&cs)[8], const float (&sn)[8], float eps) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (norm) {
+        const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = rbf(w[j] * rbf(x[j] * r));
+    }
+    if (rope) {
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = __shfl_xor(x[j], 8, 64);   // rotate-half partner d ± 64
+        if (norm) {
+            const float sg = li < 8 ? -1.0f : 1.0f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = rbf(x[j] * cs[j]) + rbf(sg * p[j] * sn[j]);
+        }
+    }
+}
+
+// destination row of head `u` (q | k | v order) for token (b, s); nullptr for u past the end
+__device__ __forceinline__ bf16_t *head_dst(const HeadPostArgs &a, int u, int b, int s, const bf16_t *&nw) {
+    nw = nullptr;
+    if (u < a.nq) {
+        nw = a.qw;
+        return a.q + (((int64_t)b * a.nq + u) * a.S_dst + s) * 128;
+    }
+    if (u < a.nq + a.nk) {
+        nw = a.kw;
+        return a.k + (((int64_t)b * a.nk + (u - a.nq)) * a.S_dst + s) * 128;
+    }
+    if (u < a.nq + a.nk + a.nv) return a.v + (((int64_t)b * a.nv + (u - a.nq - a.nk)) * a.S_dst + s) * 128;
+    return nullptr;
+}
+
+}  // namespace acehip

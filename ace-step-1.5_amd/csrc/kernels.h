@@ -5,12 +5,26 @@
 namespace acehip {
 
 // ------------------------------------------------------------------ GEMM ---
+// per-head post-projection: q/k RMSNorm (+RoPE) and scatter to head-major layouts
+struct HeadPostArgs {
+    const bf16_t *src; int64_t ld_src;   // rows [B*S]
+    int B, S;
+    int nq, nk, nv;                      // heads of each kind in the row (q | k | v)
+    const bf16_t *qw, *kw;               // norm weights [128]
+    const bf16_t *cos, *sin;             // [S][128] bf16 or null (no RoPE)
+    bf16_t *q, *k, *v;                   // [B][nq|nk|nv][S_dst][128]
+    int S_dst;
+    float eps;
+};
 enum GemmEpi {
     EPI_STORE = 0,       // C = bf16(acc + bias)
     EPI_GATED_RES = 1,   // C = bf16(res + bf16(bf16(acc) * gate[b][n]))   (AdaLN-Zero gated residual)
     EPI_RES = 2,         // C = bf16(res + bf16(acc))                       (plain residual)
     EPI_SWIGLU = 3,      // packed [gate|up] blocks of 32 rows → C[M, N/2] = bf16(silu(g)·u)
+    EPI_HEADPOST = 4,    // bf16(acc) staged in LDS, then per-128-column head: q/k RMSNorm (+RoPE) and
+                         // scatter to head-major [B][heads][S][128] (GemmArgs::hp); C unused
 };
+
 
 struct GemmArgs {
     const bf16_t *A; int64_t lda;   // [M, K]
@@ -21,6 +35,7 @@ struct GemmArgs {
     const bf16_t *bias;             // [N] or null
     const bf16_t *res; int64_t ldr; // residual (may alias C)
     const bf16_t *gate; int64_t gate_bstride; int rows_per_batch;
+    HeadPostArgs hp;                // EPI_HEADPOST only (rows of hp.B·hp.S; hp.src/ld_src unused)
 };
 int gemm(const GemmArgs &a, hipStream_t s);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
@@ -48,20 +63,10 @@ int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16
 // out[m] = AdaLN or plain RMSNorm of x[m] (rows of D):
 //   plain: bf16(w · bf16(x·rsqrt(mean x²+eps)))
 //   mod:   bf16(bf16(plain · bf16(1+scale[b])) + shift[b])
+void rmsnorm_set_rows(int rows_per_wave);   // 0 = default
 int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
                 hipStream_t s);
-// per-head post-projection: q/k RMSNorm (+RoPE) and scatter to head-major layouts
-struct HeadPostArgs {
-    const bf16_t *src; int64_t ld_src;   // rows [B*S]
-    int B, S;
-    int nq, nk, nv;                      // heads of each kind in the row (q | k | v)
-    const bf16_t *qw, *kw;               // norm weights [128]
-    const bf16_t *cos, *sin;             // [S][128] bf16 or null (no RoPE)
-    bf16_t *q, *k, *v;                   // [B][nq|nk|nv][S_dst][128]
-    int S_dst;
-    float eps;
-};
 int head_post(const HeadPostArgs &a, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---

@@ -5,18 +5,39 @@
 // norm_out :1496), reproducing each bf16 rounding of the torch op sequence:
 //   n = bf16(x·rsqrt(mean(x²)+eps)); y = bf16(w·n);
 //   y = bf16(y·bf16(1+scale)); y = bf16(y+shift)
-// One wave per row, 16-byte vector loads (HBM-bound: 2·D bytes in, 2·D out).
+// R rows per wave, 16-byte vector loads (HBM-bound: 2·D bytes in, 2·D out).
 //
 // head_post: after the fused QKV GEMM, each 128-wide head gets its RMSNorm
 // (q_norm / k_norm, base:304,338), RoPE rotate-half with bf16 rounding of
 // q·cos, rot(q)·sin and the sum (modeling_qwen3.py:166-170), and is scattered
 // into the head-major [B][heads][S][128] layout the attention kernel streams.
 #include "kernels.h"
+#include "headpost.h"
 
 namespace acehip {
 namespace {
 
-template <int V, int NV>   // elements per vector access (8 → 16 B, 4 → 8 B); vectors per lane (D = 64·V·NV)
+template <int V> struct VecOf;
+template <> struct VecOf<8> { typedef uint4 T; };
+template <> struct VecOf<4> { typedef uint2 T; };
+
+template <int V>
+__device__ __forceinline__ void unpackv(const typename VecOf<V>::T &u, float *f) {
+    if constexpr (V == 8) unpack8(u, f);
+    else unpack4(u, f);
+}
+template <int V>
+__device__ __forceinline__ typename VecOf<V>::T packv(const float *f) {
+    if constexpr (V == 8) return pack8(f);
+    else return pack4(f);
+}
+
+// V elements per vector access (8 → 16 B, 4 → 8 B), NV vectors per lane
+// (D = 64·V·NV), R consecutive rows per wave: the R rows' loads are all in
+// flight before the first reduction, and the norm weight / AdaLN scale+shift
+// vectors are loaded once per wave (re-loaded only when the rows cross a
+// batch boundary).
+template <int V, int NV, int R>
 __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restrict__ x,
                                                           const bf16_t *__restrict__ w,
                                                           const bf16_t *__restrict__ shift,
@@ -24,62 +45,141 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
                                                           int64_t mod_bstride, int rows_per_batch,
                                                           bf16_t *__restrict__ out, int M, int D,
                                                           float eps) {
+    typedef typename VecOf<V>::T vec_t;
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;
-    const bf16_t *xr = x + (int64_t)row * D;
-    constexpr int MAXV = NV;
-    float v[MAXV][V];
-    constexpr int nv = NV;
-    float ss = 0.f;
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+    if (row0 >= M) return;
+    vec_t xr[R][NV];
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-        if (i < nv) {
-            const int e = (i * 64 + lane) * V;
-            if constexpr (V == 8) unpack8(*(const uint4 *)(xr + e), v[i]);
-            else unpack4(*(const uint2 *)(xr + e), v[i]);
+    for (int r = 0; r < R; ++r) {
+        const bf16_t *xp = x + (int64_t)min(row0 + r, M - 1) * D;
 #pragma unroll
-            for (int j = 0; j < V; ++j) ss += v[i][j] * v[i][j];
+        for (int i = 0; i < NV; ++i) xr[r][i] = *(const vec_t *)(xp + (i * 64 + lane) * V);
+    }
+    // weight / modulation loads are independent of the reductions: issue them first
+    vec_t wr[NV], s1r[NV], s2r[NV];
+    int cur_b = row0 / rows_per_batch;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int e = (i * 64 + lane) * V;
+        wr[i] = *(const vec_t *)(w + e);
+        if (scale) {
+            s1r[i] = *(const vec_t *)(scale + (int64_t)cur_b * mod_bstride + e);
+            s2r[i] = *(const vec_t *)(shift + (int64_t)cur_b * mod_bstride + e);
         }
     }
-    const int b = row / rows_per_batch;
-    const bf16_t *sh = shift ? shift + (int64_t)b * mod_bstride : nullptr;
-    const bf16_t *sc = scale ? scale + (int64_t)b * mod_bstride : nullptr;
-    // issue the weight / modulation loads before the reduction (independent of it)
-    typedef __attribute__((ext_vector_type(V / 2))) uint32_t vec_t;
-    vec_t wr[MAXV], s1r[MAXV], s2r[MAXV];
+    float rs[R];
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-        if (i < nv) {
-            const int e = (i * 64 + lane) * V;
-            wr[i] = *(const vec_t *)(w + e);
-            if (sc) {
-                s1r[i] = *(const vec_t *)(sc + e);
-                s2r[i] = *(const vec_t *)(sh + e);
+    for (int r = 0; r < R; ++r) {
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            float f[V];
+            unpackv<V>(xr[r][i], f);
+#pragma unroll
+            for (int j = 0; j < V; ++j) ss += f[j] * f[j];
+        }
+        rs[r] = ss;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < R; ++r) rs[r] += __shfl_xor(rs[r], o, 64);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        if (row >= M) break;
+        if (scale && row / rows_per_batch != cur_b) {   // wave-uniform, rare
+            cur_b = row / rows_per_batch;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int e = (i * 64 + lane) * V;
+                s1r[i] = *(const vec_t *)(scale + (int64_t)cur_b * mod_bstride + e);
+                s2r[i] = *(const vec_t *)(shift + (int64_t)cur_b * mod_bstride + e);
             }
         }
-    }
-    ss = wave_sum(ss);
-    const float r = 1.0f / sqrtf(ss / (float)D + eps);
+        const float rn = 1.0f / sqrtf(rs[r] / (float)D + eps);
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-        if (i < nv) {
+        for (int i = 0; i < NV; ++i) {
             const int e = (i * 64 + lane) * V;
-            float wv[V], o[V];
-            if constexpr (V == 8) unpack8(*(const uint4 *)&wr[i], wv);
-            else unpack4(*(const uint2 *)&wr[i], wv);
+            float xv[V], wv[V], o[V];
+            unpackv<V>(xr[r][i], xv);
+            unpackv<V>(wr[i], wv);
 #pragma unroll
-            for (int j = 0; j < V; ++j) o[j] = rbf(wv[j] * rbf(v[i][j] * r));
-            if (sc) {
+            for (int j = 0; j < V; ++j) o[j] = rbf(wv[j] * rbf(xv[j] * rn));
+            if (scale) {
                 float s1[V], s2[V];
-                if constexpr (V == 8) { unpack8(*(const uint4 *)&s1r[i], s1); unpack8(*(const uint4 *)&s2r[i], s2); }
-                else { unpack4(*(const uint2 *)&s1r[i], s1); unpack4(*(const uint2 *)&s2r[i], s2); }
+                unpackv<V>(s1r[i], s1);
+                unpackv<V>(s2r[i], s2);
 #pragma unroll
                 for (int j = 0; j < V; ++j) o[j] = rbf(o[j] * rbf(1.0f + s1[j])) + s2[j];
             }
-            if constexpr (V == 8) *(uint4 *)(out + (int64_t)row * D + e) = pack8(o);
-            else *(uint2 *)(out + (int64_t)row * D + e) = pack4(o);
+            *(vec_t *)(out + (int64_t)row * D + e) = packv<V>(o);
         }
+    }
+}
+
+// WPR waves per row (D = 512·NV·WPR, 16-B accesses): more waves in flight
+// for the same bytes; the row's sum of squares is combined through LDS.
+template <int NV, int WPR>
+__global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *__restrict__ x,
+                                                            const bf16_t *__restrict__ w,
+                                                            const bf16_t *__restrict__ shift,
+                                                            const bf16_t *__restrict__ scale,
+                                                            int64_t mod_bstride, int rows_per_batch,
+                                                            bf16_t *__restrict__ out, int M, int D,
+                                                            float eps) {
+    constexpr int RPB = 4 / WPR;   // rows per 256-thread block
+    __shared__ float part[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int rl = wave / WPR, wp = wave % WPR;
+    const int row = min(blockIdx.x * RPB + rl, M - 1);
+    const int b = row / rows_per_batch;
+    const bf16_t *xp = x + (int64_t)row * D;
+    uint4 xr[NV], wr[NV], s1r[NV], s2r[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) xr[i] = *(const uint4 *)(xp + ((wp * NV + i) * 64 + lane) * 8);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int e = ((wp * NV + i) * 64 + lane) * 8;
+        wr[i] = *(const uint4 *)(w + e);
+        if (scale) {
+            s1r[i] = *(const uint4 *)(scale + (int64_t)b * mod_bstride + e);
+            s2r[i] = *(const uint4 *)(shift + (int64_t)b * mod_bstride + e);
+        }
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        float f[8];
+        unpack8(xr[i], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) part[wave] = ss;
+    __syncthreads();
+    ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < WPR; ++q) ss += part[rl * WPR + q];   // fixed order: identical in every wave of the row
+    if (blockIdx.x * RPB + rl >= M) return;
+    const float rn = 1.0f / sqrtf(ss / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int e = ((wp * NV + i) * 64 + lane) * 8;
+        float xv[8], wv[8], o[8];
+        unpack8(xr[i], xv);
+        unpack8(wr[i], wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rbf(wv[j] * rbf(xv[j] * rn));
+        if (scale) {
+            float s1[8], s2[8];
+            unpack8(s1r[i], s1);
+            unpack8(s2r[i], s2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = rbf(o[j] * rbf(1.0f + s1[j])) + s2[j];
+        }
+        *(uint4 *)(out + (int64_t)row * D + e) = pack8(o);
     }
 }
 
@@ -93,69 +193,35 @@ __global__ __launch_bounds__(256) void head_post_kernel(HeadPostArgs a) {
     const int units = a.nq + a.nk + a.nv;
     const bf16_t *src = a.src + (int64_t)row * a.ld_src;
     const int d = li * 8;
-    float cs[8], sn[8];
+    float cs[8] = {}, sn[8] = {};
     if (a.cos) {
         unpack8(*(const uint4 *)(a.cos + (int64_t)s * 128 + d), cs);
         unpack8(*(const uint4 *)(a.sin + (int64_t)s * 128 + d), sn);
     }
     for (int u0 = wave * 4; u0 < units; u0 += 16) {
         const int u = u0 + sub;
-        const bool act = u < units;
-        float x[8];
-        if (act) unpack8(*(const uint4 *)(src + u * 128 + d), x);
-        else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = 0.f;
-        bf16_t *dst = nullptr;
-        const bf16_t *nw = nullptr;
-        if (u < a.nq) {
-            dst = a.q + (((int64_t)b * a.nq + u) * a.S_dst + s) * 128;
-            nw = a.qw;
-        } else if (u < a.nq + a.nk) {
-            dst = a.k + (((int64_t)b * a.nk + (u - a.nq)) * a.S_dst + s) * 128;
-            nw = a.kw;
-        } else if (act) {
-            dst = a.v + (((int64_t)b * a.nv + (u - a.nq - a.nk)) * a.S_dst + s) * 128;
-        }
-        // per-head RMSNorm over 16 lanes (all lanes shuffle; inactive ones carry zeros)
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-        if (nw) {
-            const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + a.eps);
-            float w[8];
-            unpack8(*(const uint4 *)(nw + d), w);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = rbf(w[j] * rbf(x[j] * r));
-        }
-        if (a.cos) {
-            float p[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) p[j] = __shfl_xor(x[j], 8, 64);
-            if (nw) {
-                const float sg = li < 8 ? -1.0f : 1.0f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x[j] = rbf(x[j] * cs[j]) + rbf(sg * p[j] * sn[j]);
-            }
-        }
-        if (act) *(uint4 *)(dst + d) = pack8(x);
+        float x[8] = {};
+        if (u < units) unpack8(*(const uint4 *)(src + u * 128 + d), x);
+        const bf16_t *nw;
+        bf16_t *dst = head_dst(a, u, b, s, nw);
+        float w[8] = {};
+        if (nw) unpack8(*(const uint4 *)(nw + d), w);
+        head_norm_rope(x, li, nw != nullptr, w, a.cos != nullptr, cs, sn, a.eps);
+        if (dst) *(uint4 *)(dst + d) = pack8(x);
     }
 }
 
 }  // namespace
 
-int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
-                int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
-                hipStream_t s) {
-    if (M <= 0) return 0;
-    if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
-    if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
-    const int grid = (M + 3) / 4;
-    const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
-#define RMS_LAUNCH(V_, NV_)                                                                        \
-    rmsnorm_mod_kernel<V_, NV_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps)
+static int g_rms_rows = 0;   // rows per wave override (tests / micro-bench); 0 = default
+void rmsnorm_set_rows(int r) { g_rms_rows = r; }
+
+template <int R>
+static void rms_launch(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
+                       int64_t mbs, int rpb, bf16_t *out, int M, int D, float eps, hipStream_t s) {
+    const int grid = (M + 4 * R - 1) / (4 * R);
+#define RMS_LAUNCH(V_, NV_) \
+    rmsnorm_mod_kernel<V_, NV_, R><<<grid, 256, 0, s>>>(x, w, shift, scale, mbs, rpb, out, M, D, eps)
     if (D % 512 == 0) {
         switch (D / 512) {
             case 1: RMS_LAUNCH(8, 1); break;
@@ -180,6 +246,34 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
         }
     }
 #undef RMS_LAUNCH
+}
+
+int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
+                int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
+                hipStream_t s) {
+    if (M <= 0) return 0;
+    if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
+    if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
+    const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
+    const int R = g_rms_rows ? g_rms_rows : 1;
+    if (R < 0 && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
+        const int WPR = -R, nv = D / (512 * WPR), grid = (M + 4 / WPR - 1) / (4 / WPR);
+#define SPLIT(NV_, W_) \
+    rmsnorm_split_kernel<NV_, W_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps)
+        if (WPR == 2) {
+            if (nv == 1) SPLIT(1, 2); else if (nv == 2) SPLIT(2, 2); else if (nv == 3) SPLIT(3, 2); else SPLIT(4, 2);
+        } else {
+            if (nv == 1) SPLIT(1, 4); else if (nv == 2) SPLIT(2, 4); else if (nv == 3) SPLIT(3, 4); else SPLIT(4, 4);
+        }
+#undef SPLIT
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+    switch (R < 0 ? 1 : R) {
+        case 1: rms_launch<1>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
+        case 2: rms_launch<2>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
+        default: rms_launch<4>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
+    }
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -206,6 +206,23 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H,
                           int KV, int Sq, int Sk, int window, float scale, void *stream);
 
+/* Qwen3RMSNorm (+ AdaLN modulation when shift/scale are given) over rows of D
+ * (transformers modeling_qwen3.py:59-64; reference base:499,530,1496):
+ * out = bf16(bf16(bf16(w·bf16(x·rsqrt(mean x²+eps)))·bf16(1+scale[b])) + shift[b]),
+ * b = row / rows_per_batch, shift/scale rows mod_bstride apart.
+ * rows_per_wave: 0 = default, 1/2/4 rows per wave, -2/-4 = 2/4 waves per row (tuning, tests). */
+int acehip_rmsnorm_bf16(const void *x, const void *w, const void *shift, const void *scale,
+                        int64_t mod_bstride, int rows_per_batch, void *out, int M, int D, float eps,
+                        int rows_per_wave, void *stream);
+
+/* Projection GEMM with the q/k RMSNorm + RoPE + head-major scatter epilogue
+ * (reference base:300-345 q_proj/k_proj/v_proj → q_norm/k_norm → apply_rotary_pos_emb):
+ * rows [B·S] of A · W[N,K]ᵀ, N = (nq+nk+nv)·128, split into heads q | k | v and written
+ * to q [B,nq,S,128], k [B,nk,S,128], v [B,nv,S,128]; cos/sin [S,128] or NULL (no RoPE). */
+int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int B, int S, int nq,
+                              int nk, int nv, const void *qw, const void *kw, const void *cos,
+                              const void *sin, float eps, void *q, void *k, void *v, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
