@@ -170,6 +170,61 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     }
 }
 
+// Epilogue of one wave's SM×SN grid of 16×16 sub-tiles: lane (fr, fc) owns row
+// row0 + 16i + fr and columns col0 + 16j + 4fc .. +3 (the transposed MFMA tile).
+// SwiGLU: the wave's columns are whole 64-column panels [32 gate | 32 up].
+template <int SM, int SN, int EPI>
+__device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&acc)[SM][SN], int row0, int col0,
+                                              int fr, int fc) {
+#pragma unroll
+    for (int i = 0; i < SM; ++i) {
+        const int m = row0 + i * 16 + fr;
+        if (m >= a.M) continue;
+        if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+            for (int pnl = 0; pnl < SN / 4; ++pnl)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int nout = ((col0 + pnl * 64) >> 1) + j * 16 + fc * 4;
+                    float o[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float g = rbf(acc[i][4 * pnl + j][r]);
+                        const float u = rbf(acc[i][4 * pnl + j + 2][r]);
+                        o[r] = rbf(silu_f(g)) * u;
+                    }
+                    *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
+                }
+        } else {
+            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
+#pragma unroll
+            for (int j = 0; j < SN; ++j) {
+                const int n = col0 + j * 16 + fc * 4;
+                float o[4];
+                if constexpr (EPI == EPI_STORE) {
+                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + bb[r];
+                } else {
+                    float rr[4];
+                    unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + n), rr);
+                    if constexpr (EPI == EPI_GATED_RES) {
+                        float gg[4];
+                        unpack4(*(const uint2 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[i][j][r]) * gg[r]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[i][j][r]);
+                    }
+                }
+                *(uint2 *)(a.C + (int64_t)m * a.ldc + n) = pack4(o);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Ping-pong variant: BM×256 tile, 8 waves as 2 groups (wr = 0/1, A rows
 // [wr·BM/2, +BM/2)) × 4 (64 columns each).  The groups run one barrier apart,
@@ -380,52 +435,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         return;
     }
 
-    // epilogue: lane owns row m, columns n..n+3 of each 16x16 sub-tile
-#pragma unroll
-    for (int i = 0; i < SM; ++i) {
-        const int m = m0 + arow + i * 16 + fr;
-        if (m >= a.M) continue;
-        if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int nout = ((n0 + wc * 64) >> 1) + j * 16 + fc * 4;
-                float o[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float g = rbf(acc[i][j][r]);
-                    const float u = rbf(acc[i][j + 2][r]);
-                    o[r] = rbf(silu_f(g)) * u;
-                }
-                *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
-            }
-        } else {
-            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int n = n0 + wc * 64 + j * 16 + fc * 4;
-                float o[4];
-                if constexpr (EPI == EPI_STORE) {
-                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
-                    if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + bb[r];
-                } else {
-                    float rr[4];
-                    unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + n), rr);
-                    if constexpr (EPI == EPI_GATED_RES) {
-                        float gg[4];
-                        unpack4(*(const uint2 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[i][j][r]) * gg[r]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[i][j][r]);
-                    }
-                }
-                *(uint2 *)(a.C + (int64_t)m * a.ldc + n) = pack4(o);
-            }
-        }
-    }
+    epilogue_tile<SM, 4, EPI>(a, acc, m0 + arow, n0 + wc * 64, fr, fc);
 }
 
 template <int BM>
