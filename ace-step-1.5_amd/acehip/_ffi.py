@@ -26,7 +26,9 @@ EXPORTS = [
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
     "acehip_vae_encode", "acehip_vae_destroy",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
-    "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16",
+    "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16", "acehip_attention_masked_bf16",
+    "acehip_enc_create", "acehip_enc_set_weight", "acehip_enc_finalize", "acehip_enc_embed",
+    "acehip_enc_forward", "acehip_enc_destroy",
 ]
 
 
@@ -36,6 +38,13 @@ class DiTCfg(ctypes.Structure):
                 ("in_channels", c_int), ("out_channels", c_int), ("eps", c_float),
                 ("rope_theta", c_float), ("max_S", c_int), ("max_Bc", c_int), ("max_Lenc", c_int),
                 ("sliding", POINTER(c_uint8))]
+
+
+class EncCfg(ctypes.Structure):
+    _fields_ = [("hidden", c_int), ("intermediate", c_int), ("heads", c_int), ("kv_heads", c_int),
+                ("head_dim", c_int), ("layers", c_int), ("window", c_int), ("in_dim", c_int),
+                ("embed_bias", c_int), ("out_dim", c_int), ("eps", c_float), ("rope_theta", c_float),
+                ("max_tokens", c_int), ("max_S", c_int), ("sliding", POINTER(c_uint8))]
 
 
 class VAECfg(ctypes.Structure):
@@ -77,6 +86,14 @@ def _declare(lib):
                                         c_int, P]),
         "acehip_attention_bf16": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                           c_float, P]),
+        "acehip_attention_masked_bf16": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                                 c_float, P, P]),
+        "acehip_enc_create": (c_int, [c_int, POINTER(EncCfg), POINTER(c_void_p)]),
+        "acehip_enc_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
+        "acehip_enc_finalize": (c_int, [P]),
+        "acehip_enc_embed": (c_int, [P, P, c_int, P, P]),
+        "acehip_enc_forward": (c_int, [P, P, P, c_int, c_int, P, P]),
+        "acehip_enc_destroy": (c_int, [P]),
         "acehip_rmsnorm_bf16": (c_int, [P, P, P, P, c_int64, c_int, P, c_int, c_int, c_float, c_int, P]),
         "acehip_gemm_headpost_bf16": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                               P, P, P, P, c_float, P, P, P, P]),

@@ -1,0 +1,258 @@
+"""Condition encoders on the HIP path: the ``AceStepConditionEncoder`` drop-in
+and a ``prepare_condition`` drop-in built on it.
+
+``ConditionEncoder.__call__`` keeps the contract of the reference
+``AceStepConditionEncoder.forward`` (``acestep/models/base/
+modeling_acestep_v15_base.py:1527-1554``): text projector, lyric encoder
+(:577-731, key-padding masked), timbre encoder (:997-1178) and the two
+``pack_sequences`` (:138-169) → ``(encoder_hidden_states, encoder_attention_mask)``.
+Every Linear / encoder layer / norm runs in libacehip (``acehip_enc_*``,
+``acehip_gemm_bf16``); the timbre unpack and ``pack_sequences`` are index
+plumbing (stable argsort + gather) done with torch ops on the device, exactly
+as the reference does them.  There is no CPU or eager fallback.
+
+``HipPrepareCondition`` mirrors ``prepare_condition`` (base:1607-1652) for
+the text2music / repaint cases (no audio-code hints needed, or precomputed
+hints given).  Cover songs that need the FSQ audio tokenizer
+(``vector_quantize_pytorch.ResidualFSQ``, not built here — SURVEY §8f row 2)
+are routed to the reference's own ``prepare_condition`` when one is given,
+otherwise they raise.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+
+from . import _ffi
+from ._ffi import ACEHIP_BF16, ACEHIP_F32, check, lib, ptr, shape_arg, stream_ptr
+from .config import DiTConfig
+
+
+class EncoderStack:
+    """One ``acehip_enc`` handle: embed_tokens → AceStepEncoderLayer × n →
+    norm (→ proj_out), reference base:374-440."""
+
+    def __init__(self, cfg: DiTConfig, n_layers: int, in_dim: int, embed_bias: bool = True,
+                 out_dim: int = 0, device: int = 0, max_tokens: int = 8192, max_S: int = 4096):
+        self.cfg = cfg
+        self.device = torch.device("cuda", device)
+        self.D = cfg.hidden_size
+        self.out_dim = out_dim
+        self.max_tokens, self.max_S = max_tokens, max_S
+        sl = (_ffi.c_uint8 * max(n_layers, 1))(*[1 if cfg.is_sliding(i) else 0 for i in range(n_layers)])
+        self._sliding = sl
+        c = _ffi.EncCfg(hidden=cfg.hidden_size, intermediate=cfg.intermediate_size,
+                        heads=cfg.num_attention_heads, kv_heads=cfg.num_key_value_heads,
+                        head_dim=cfg.head_dim, layers=n_layers, window=cfg.sliding_window, in_dim=in_dim,
+                        embed_bias=1 if embed_bias else 0, out_dim=out_dim, eps=cfg.rms_norm_eps,
+                        rope_theta=cfg.rope_theta, max_tokens=max_tokens, max_S=max_S,
+                        sliding=_ffi.ctypes.cast(sl, _ffi.POINTER(_ffi.c_uint8)))
+        h = _ffi.c_void_p()
+        check(lib().acehip_enc_create(device, _ffi.ctypes.byref(c), _ffi.ctypes.byref(h)), "enc_create")
+        self.h = h
+        self.extra: Dict[str, torch.Tensor] = {}   # special_token(s): host-side plumbing parameters
+
+    def set_weight(self, name: str, t: torch.Tensor):
+        t = t.detach().contiguous()
+        if t.dtype not in (torch.float32, torch.bfloat16):
+            t = t.float()
+        dt = ACEHIP_F32 if t.dtype == torch.float32 else ACEHIP_BF16
+        check(lib().acehip_enc_set_weight(self.h, name.encode(), ptr(t), dt, t.dim(), shape_arg(tuple(t.shape)),
+                                          1 if t.is_cuda else 0), f"enc_set_weight({name})")
+
+    def load(self, weights: Dict[str, torch.Tensor], prefix: str = ""):
+        """Module-local reference names under ``prefix`` (e.g. ``lyric_encoder.``)."""
+        hd = self.cfg.head_dim
+        inv = 1.0 / (self.cfg.rope_theta ** (torch.arange(0, hd, 2, dtype=torch.float) / hd))
+        self.set_weight("_rope_inv_freq", inv)
+        for k, v in weights.items():
+            if not k.startswith(prefix):
+                continue
+            k = k[len(prefix):]
+            if k.startswith("rotary_emb."):
+                continue
+            if k in ("special_token", "special_tokens"):
+                self.extra[k] = v.detach().to(self.device, torch.bfloat16)
+                continue
+            self.set_weight(k, v)
+        check(lib().acehip_enc_finalize(self.h), "enc_finalize")
+
+    def embed(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.to(self.device, torch.bfloat16).contiguous()
+        M = x.numel() // x.shape[-1]
+        out = torch.empty(*x.shape[:-1], self.D, device=self.device, dtype=torch.bfloat16)
+        check(lib().acehip_enc_embed(self.h, ptr(x), M, ptr(out), stream_ptr()), "enc_embed")
+        return out
+
+    def forward(self, h: torch.Tensor, kmask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """h [B, S, D] bf16 (embedded) → [B, S, out_dim or D]; kmask [B, S] (1 = attend) or None."""
+        h = h.to(self.device, torch.bfloat16).contiguous()
+        B, S, _ = h.shape
+        km = None
+        if kmask is not None:
+            km = (kmask != 0).to(device=self.device, dtype=torch.uint8).contiguous()
+        out = torch.empty(B, S, self.out_dim or self.D, device=self.device, dtype=torch.bfloat16)
+        check(lib().acehip_enc_forward(self.h, ptr(h), ptr(km), B, S, ptr(out), stream_ptr()), "enc_forward")
+        self._keep = (h, km)   # inputs stay alive until the stream consumed them
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().acehip_enc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def unpack_timbre(emb: torch.Tensor, order: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """AceStepTimbreEncoder.unpack_timbre_embeddings (base:1023-1073): packed rows
+    [N, d] → [B, max_count, d] by batch id in packed order, mask [B, max_count] long.
+    (The reference's one-hot matmul places each row exactly; an index scatter
+    is the same result.)"""
+    N, d = emb.shape
+    dev = emb.device
+    order = order.to(dev).long()
+    B = int(order.max().item()) + 1
+    counts = torch.bincount(order, minlength=B)
+    max_count = int(counts.max().item())
+    sorted_idx = torch.argsort(order * N + torch.arange(N, device=dev), stable=True)
+    starts = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(counts, 0)[:-1]])
+    pos_sorted = torch.arange(N, device=dev) - starts[order[sorted_idx]]
+    pos = torch.empty_like(pos_sorted)
+    pos[sorted_idx] = pos_sorted
+    out = torch.zeros(B * max_count, d, device=dev, dtype=emb.dtype)
+    out[order * max_count + pos] = emb
+    mask = torch.zeros(B * max_count, dtype=torch.long, device=dev)
+    mask[order * max_count + pos] = 1
+    return out.view(B, max_count, d), mask.view(B, max_count)
+
+
+def pack_sequences(h1, h2, m1, m2):
+    """pack_sequences (base:138-169): valid tokens first (stable), prefix mask."""
+    h = torch.cat([h1, h2], dim=1)
+    m = torch.cat([m1.to(h.device), m2.to(h.device)], dim=1)
+    B, L, D = h.shape
+    idx = m.argsort(dim=1, descending=True, stable=True)
+    out = torch.gather(h, 1, idx.unsqueeze(-1).expand(B, L, D))
+    lengths = m.sum(dim=1)
+    return out, torch.arange(L, device=h.device)[None, :] < lengths[:, None]
+
+
+class ConditionEncoder:
+    """Drop-in for ``AceStepConditionEncoder`` (base:1509-1554) on libacehip."""
+
+    def __init__(self, cfg: DiTConfig, device: int = 0, max_batch: int = 8, max_lyric: int = 4096,
+                 max_refs: int = 8, max_ref_frames: int = 750):
+        self.cfg = cfg
+        self.device = torch.device("cuda", device)
+        self.lyric = EncoderStack(cfg, cfg.num_lyric_encoder_hidden_layers, cfg.text_hidden_dim, True,
+                                  device=device, max_tokens=max_batch * max_lyric, max_S=max_lyric)
+        self.timbre = EncoderStack(cfg, cfg.num_timbre_encoder_hidden_layers, cfg.timbre_hidden_dim, True,
+                                   device=device, max_tokens=max_refs * max_ref_frames, max_S=max_ref_frames)
+        self.w_text: Optional[torch.Tensor] = None
+
+    @classmethod
+    def from_reference_model(cls, model, **kw) -> "ConditionEncoder":
+        """From a loaded ``AceStepConditionGenerationModel`` (its ``encoder`` submodule)."""
+        c = model.config
+        cfg = DiTConfig(hidden_size=c.hidden_size, intermediate_size=c.intermediate_size,
+                        num_hidden_layers=c.num_hidden_layers, num_attention_heads=c.num_attention_heads,
+                        num_key_value_heads=c.num_key_value_heads, head_dim=c.head_dim,
+                        sliding_window=c.sliding_window, rms_norm_eps=c.rms_norm_eps,
+                        rope_theta=float(getattr(c, "rope_theta", 1e6)), layer_types=list(c.layer_types),
+                        num_lyric_encoder_hidden_layers=c.num_lyric_encoder_hidden_layers,
+                        num_timbre_encoder_hidden_layers=c.num_timbre_encoder_hidden_layers,
+                        text_hidden_dim=c.text_hidden_dim, timbre_hidden_dim=c.timbre_hidden_dim)
+        dev = next(model.parameters()).device
+        ce = cls(cfg, dev.index or 0, **kw)
+        ce.load(model.encoder.state_dict())
+        return ce
+
+    def load(self, weights: Dict[str, torch.Tensor]):
+        w = {(k[len("encoder."):] if k.startswith("encoder.") else k): v for k, v in weights.items()}
+        self.w_text = w["text_projector.weight"].detach().to(self.device, torch.bfloat16).contiguous()
+        self.lyric.load(w, "lyric_encoder.")
+        self.timbre.load(w, "timbre_encoder.")
+
+    def text_projector(self, text: torch.Tensor) -> torch.Tensor:
+        """nn.Linear(text_hidden_dim → hidden, bias=False) (base:1521, :1540)."""
+        x = text.to(self.device, torch.bfloat16).contiguous()
+        M, K = x.numel() // x.shape[-1], x.shape[-1]
+        N = self.w_text.shape[0]
+        out = torch.empty(*x.shape[:-1], N, device=self.device, dtype=torch.bfloat16)
+        check(lib().acehip_gemm_bf16(ptr(x), K, ptr(self.w_text), K, ptr(out), N, M, N, K, None, stream_ptr()),
+              "text_projector")
+        return out
+
+    def lyric_encoder(self, lyric_hidden_states, lyric_attention_mask):
+        """AceStepLyricEncoder.forward (base:603-731) → last_hidden_state."""
+        return self.lyric.forward(self.lyric.embed(lyric_hidden_states), lyric_attention_mask)
+
+    def timbre_encoder(self, packed, order):
+        """AceStepTimbreEncoder.forward (base:1076-1178): no padding mask, row 0."""
+        h = self.timbre.forward(self.timbre.embed(packed), None)
+        return unpack_timbre(h[:, 0, :], order)
+
+    def __call__(self, text_hidden_states, text_attention_mask, lyric_hidden_states, lyric_attention_mask,
+                 refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask):
+        dev = self.device
+        text = self.text_projector(text_hidden_states)
+        lyric = self.lyric_encoder(lyric_hidden_states, lyric_attention_mask)
+        timbre, timbre_mask = self.timbre_encoder(refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask)
+        enc, mask = pack_sequences(lyric, timbre, lyric_attention_mask.to(dev), timbre_mask)
+        return pack_sequences(enc, text, mask, text_attention_mask.to(dev))
+
+    forward = __call__
+
+    def close(self):
+        self.lyric.close()
+        self.timbre.close()
+
+
+class HipPrepareCondition:
+    """Drop-in for ``AceStepConditionGenerationModel.prepare_condition``
+    (base:1607-1652) with the encoders on libacehip.
+
+    The reference always runs the audio tokenizer/detokenizer and then keeps
+    its output only where ``is_covers > 0`` (base:1645-1649); without covers
+    (or with ``precomputed_lm_hints_25Hz``) that work is dead and skipped here.
+    Covers that need the tokenizer go to ``fallback`` (the reference's own
+    ``prepare_condition``) or raise."""
+
+    def __init__(self, encoder: ConditionEncoder, fallback: Optional[Callable] = None):
+        self.encoder = encoder
+        self.fallback = fallback
+
+    def __call__(self, text_hidden_states, text_attention_mask, lyric_hidden_states, lyric_attention_mask,
+                 refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask, hidden_states,
+                 attention_mask, silence_latent, src_latents, chunk_masks, is_covers,
+                 precomputed_lm_hints_25Hz=None, audio_codes=None):
+        need_tokenizer = precomputed_lm_hints_25Hz is None and (
+            audio_codes is not None or bool((is_covers > 0).any()))
+        if need_tokenizer:
+            if self.fallback is None:
+                raise NotImplementedError("acehip: cover conditioning needs the FSQ audio tokenizer "
+                                          "(pass precomputed_lm_hints_25Hz or a reference fallback)")
+            return self.fallback(
+                text_hidden_states=text_hidden_states, text_attention_mask=text_attention_mask,
+                lyric_hidden_states=lyric_hidden_states, lyric_attention_mask=lyric_attention_mask,
+                refer_audio_acoustic_hidden_states_packed=refer_audio_acoustic_hidden_states_packed,
+                refer_audio_order_mask=refer_audio_order_mask, hidden_states=hidden_states,
+                attention_mask=attention_mask, silence_latent=silence_latent, src_latents=src_latents,
+                chunk_masks=chunk_masks, is_covers=is_covers,
+                precomputed_lm_hints_25Hz=precomputed_lm_hints_25Hz, audio_codes=audio_codes)
+        dtype = hidden_states.dtype
+        enc, enc_mask = self.encoder(text_hidden_states, text_attention_mask, lyric_hidden_states,
+                                     lyric_attention_mask, refer_audio_acoustic_hidden_states_packed,
+                                     refer_audio_order_mask)
+        if precomputed_lm_hints_25Hz is not None:
+            hints = precomputed_lm_hints_25Hz[:, :src_latents.shape[1], :]
+            src_latents = torch.where(is_covers.view(-1, 1, 1) > 0, hints, src_latents)
+        ctx = torch.cat([src_latents, chunk_masks.to(dtype)], dim=-1)
+        return enc.to(dtype), enc_mask, ctx

@@ -27,13 +27,24 @@ class DiTConfig:
     rms_norm_eps: float = 1e-6
     rope_theta: float = 1_000_000.0
     layer_types: Optional[List[str]] = None
+    # condition encoders (configuration_acestep_v15.py:173-185)
+    num_lyric_encoder_hidden_layers: int = 8
+    num_timbre_encoder_hidden_layers: int = 4
+    num_attention_pooler_hidden_layers: int = 2
+    text_hidden_dim: int = 1024
+    timbre_hidden_dim: int = 64
+    pool_window_size: int = 5
 
     def __post_init__(self):
         if self.layer_types is None:
-            # configuration_acestep_v15.py:250-254 — even index sliding, odd full
+            # configuration_acestep_v15.py:250-254 — even index sliding, odd full.  The
+            # encoders index the same list by their own layer index (base:399), so it
+            # must cover the deepest stack.
+            n = max(self.num_hidden_layers, self.num_lyric_encoder_hidden_layers,
+                    self.num_timbre_encoder_hidden_layers, self.num_attention_pooler_hidden_layers)
             self.layer_types = [
                 "sliding_attention" if (i + 1) % 2 else "full_attention"
-                for i in range(self.num_hidden_layers)
+                for i in range(n)
             ]
 
     @property

@@ -64,6 +64,52 @@ def dit_weight_shapes(cfg: DiTConfig) -> Dict[str, Shape]:
     return s
 
 
+def encoder_stack_shapes(cfg: DiTConfig, prefix: str, n_layers: int, in_dim: int, embed_bias: bool,
+                         out_dim: int = 0) -> Dict[str, Shape]:
+    """One AceStepEncoderLayer stack (base:374-440) with embed_tokens / norm /
+    optional proj_out, module-local names under ``prefix``."""
+    D, F_, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    qd, kvd = cfg.q_dim, cfg.kv_dim
+    s: Dict[str, Shape] = {f"{prefix}.embed_tokens.weight": (D, in_dim)}
+    if embed_bias:
+        s[f"{prefix}.embed_tokens.bias"] = (D,)
+    for i in range(n_layers):
+        p = f"{prefix}.layers.{i}"
+        s[f"{p}.input_layernorm.weight"] = (D,)
+        s[f"{p}.post_attention_layernorm.weight"] = (D,)
+        s[f"{p}.self_attn.q_proj.weight"] = (qd, D)
+        s[f"{p}.self_attn.k_proj.weight"] = (kvd, D)
+        s[f"{p}.self_attn.v_proj.weight"] = (kvd, D)
+        s[f"{p}.self_attn.o_proj.weight"] = (D, qd)
+        s[f"{p}.self_attn.q_norm.weight"] = (hd,)
+        s[f"{p}.self_attn.k_norm.weight"] = (hd,)
+        s[f"{p}.mlp.gate_proj.weight"] = (F_, D)
+        s[f"{p}.mlp.up_proj.weight"] = (F_, D)
+        s[f"{p}.mlp.down_proj.weight"] = (D, F_)
+    s[f"{prefix}.norm.weight"] = (D,)
+    if out_dim:
+        s[f"{prefix}.proj_out.weight"] = (out_dim, D)
+        s[f"{prefix}.proj_out.bias"] = (out_dim,)
+    return s
+
+
+def condenc_weight_shapes(cfg: DiTConfig) -> Dict[str, Shape]:
+    """AceStepConditionEncoder (base:1517-1525) module-local names: text_projector
+    (no bias), lyric_encoder (embed with bias), timbre_encoder (embed with bias,
+    special_token unused at inference, base:1087)."""
+    s: Dict[str, Shape] = {"text_projector.weight": (cfg.hidden_size, cfg.text_hidden_dim)}
+    s.update(encoder_stack_shapes(cfg, "lyric_encoder", cfg.num_lyric_encoder_hidden_layers,
+                                  cfg.text_hidden_dim, True))
+    s.update(encoder_stack_shapes(cfg, "timbre_encoder", cfg.num_timbre_encoder_hidden_layers,
+                                  cfg.timbre_hidden_dim, True))
+    s["timbre_encoder.special_token"] = (1, 1, cfg.hidden_size)
+    return s
+
+
+def synth_condenc_weights(cfg: DiTConfig, seed: int = 0, mode: str = "bench", **kw):
+    return synth_weights(condenc_weight_shapes(cfg), seed, mode, **kw)
+
+
 def vae_weight_shapes(cfg: VAEConfig, with_encoder: bool = True) -> Dict[str, Shape]:
     s: Dict[str, Shape] = {}
 

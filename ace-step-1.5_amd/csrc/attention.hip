@@ -7,7 +7,15 @@
 //     KV tiles that intersect the band are visited — the reference's SDPA
 //     path computes the full S×S and masks it),
 //   * unmasked cross-attention over the cached encoder K/V (base:1384-1428:
-//     the decoder never masks encoder padding).
+//     the decoder never masks encoder padding);
+//   * key-padding-masked self-attention for the condition encoders
+//     (AceStepEncoderLayer base:401-440 with create_4d_mask base:56-135):
+//     kmask[b][j] = 0 excludes key j.  The reference's additive mask is the
+//     finite finfo.min, so a query row with NO admissible key softmaxes
+//     uniformly over all Sk keys (band-excluded ones included); the masked
+//     mode therefore visits every KV tile and gives excluded keys a common
+//     finite score (NEG) while keys past Sk get a far lower one (PAST),
+//     which reproduces exactly that.
 //
 // Layout: q [B][H][Sq][128], k/v [B][KV][Sk][128] (head-major, written by
 // head_post), o token-major [B][Sq][o_ld] at column h·128.
@@ -24,7 +32,7 @@
 // max/sum is 32 in-register values plus one cross-half exchange.  Sᵀ's
 // accumulator registers, converted to bf16, are directly the B operand of
 // Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P).  Online softmax in the exp2 domain;
-// masked scores use a finite −1e30 sentinel (a row whose first tiles are
+// masked scores use a finite power-of-two sentinel (a row whose first tiles are
 // fully masked accumulates garbage that the first real tile's rescale zeroes).
 #include "kernels.h"
 
@@ -40,7 +48,14 @@ namespace {
 
 constexpr int QB = 128;    // queries per workgroup
 constexpr int KT = 64;     // keys per tile
-constexpr float NEG = -1e30f;
+// Sentinels are powers of two so that NEG·sl2 is exact: the exp2 argument
+// fmaf(NEG, sl2, −m) of a row whose max IS the sentinel is then exactly 0
+// (an all-masked row weighs its keys uniformly, and a row's all-masked first
+// tiles add finite garbage that the first real tile's rescale zeroes).  With a
+// non-power-of-two sentinel the fma's unrounded product differs from the
+// rounded max by up to half an ulp of 1e29 — exp2 of that is 0 or inf.
+constexpr float NEG = -0x1p100f;
+constexpr float PAST = -0x1p126f;   // masked mode: keys past Sk (never weighted, even in an all-masked row)
 
 // tail balancing: units [0, full) run whole; each later unit runs as nsplit
 // KV-range parts whose partial (O, m, l) meet in ws, merged by the last part
@@ -63,7 +78,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const bf16_t *__restrict__ v,
                                                                   bf16_t *__restrict__ o, int H, int KV,
                                                                   int Sq, int Sk, int window, float sl2,
-                                                                  int64_t o_ld, SplitArgs sp) {
+                                                                  int64_t o_ld, SplitArgs sp,
+                                                                  const uint8_t *__restrict__ kmask) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
     constexpr int NBUF = ATT_DEFER ? 3 : 2;        // K/V ring (deferred P·V still reads V(j−1))
@@ -100,7 +116,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
     const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
     int kv_lo = 0, kv_hi = Sk;
-    if (window >= 0) {
+    const uint8_t *km = kmask ? kmask + (int64_t)b * Sk : nullptr;
+    if (window >= 0 && !km) {
         kv_lo = max(0, qblk - window);
         kv_hi = min(Sk, qblk + QB + window);
     }
@@ -178,8 +195,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         if (defer && it > 0) pv(lds + ((it + NBUF - 1) % NBUF) * 2 * TILE + TILE, pf);
         // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
         // skipped (the wave still joins the barrier); one entirely inside needs no mask
-        const bool outside = window >= 0 && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window);
-        const bool interior = kv0 + KT <= Sk &&
+        const bool outside = window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window);
+        const bool interior = !km && kv0 + KT <= Sk &&
                               (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window));
         if (outside && !defer) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -214,8 +231,14 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                 for (int j = 0; j < 16; ++j) {
                     const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
                     // branch-free: window < 0 ⇒ wlim = INT_MAX
-                    const bool ok = (kj < Sk) & (abs(qi - kj) <= wlim);
-                    const float sv = ok ? st[t][j] : NEG;
+                    const bool inr = kj < Sk;
+                    bool ok = inr & (abs(qi - kj) <= wlim);
+                    float bad = NEG;
+                    if (km) {   // key-padding mode (uniform over branches: km is kernel-uniform)
+                        ok = ok && km[inr ? kj : 0] != 0;
+                        bad = inr ? NEG : PAST;
+                    }
+                    const float sv = ok ? st[t][j] : bad;
                     st[t][j] = sv;
                     mx = fmaxf(mx, sv);
                 }
@@ -333,7 +356,8 @@ size_t attention_ws_bytes() {
 }
 
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
-              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s) {
+              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s,
+              const uint8_t *kmask) {
     if (B <= 0 || Sq <= 0) return 0;
     if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
     if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
@@ -349,7 +373,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     const int tail = units % cus;
     // only long KV loops pay for the partial write + merge (measured: full attention
     // at S = 3000, 47 tiles, −27 %; band (≈7 tiles) and cross (11 tiles) lose)
-    const int unit_tiles = window >= 0 ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
+    const int unit_tiles = (window >= 0 && !kmask) ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
     if (ws && nrep == 2 && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
         sp.full = units - tail;
         sp.nsplit = min(4, cus / tail);
@@ -358,9 +382,9 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     }
     const int grid = sp.full + (units - sp.full) * sp.nsplit;
     if (nrep == 2) {
-        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
+        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else if (nrep == 1) {
-        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
+        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else {
         return fail(-1, "attention: heads/kv_heads must be 1 or 2");
     }

@@ -649,6 +649,11 @@ int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int 
 
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,
                           int Sq, int Sk, int window, float scale, void *stream) {
+    return acehip_attention_masked_bf16(q, k, v, o, B, H, KV, Sq, Sk, window, scale, nullptr, stream);
+}
+
+int acehip_attention_masked_bf16(const void *q, const void *k, const void *v, void *o, int B, int H, int KV,
+                                 int Sq, int Sk, int window, float scale, const uint8_t *kmask, void *stream) {
     // standalone entry (tests / micro-bench): one lazily allocated tail-split workspace
     // per device (the DiT runtime owns its own, allocated at create)
     static std::map<int, void *> ws_by_dev;
@@ -661,7 +666,7 @@ int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, 
         HIP_TRY(hipMemset(ws, 0, wb));
     }
     return attention((const bf16_t *)q, (const bf16_t *)k, (const bf16_t *)v, (bf16_t *)o, B, H, KV, Sq,
-                     Sk, window, scale, (int64_t)H * 128, ws, (hipStream_t)stream);
+                     Sk, window, scale, (int64_t)H * 128, ws, (hipStream_t)stream, kmask);
 }
 
 }  // extern "C"

@@ -55,6 +55,8 @@ int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj,
 // proj_in input pack: X[b][s][k*192+c] = (c<128 ? ctx : xt)[b % Bx][2s+k][..] or 0
 int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
                  hipStream_t s);
+// dst[m][0:C] = src[m][0:C] (row-strided column block copy)
+int copy_cols(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, int C, hipStream_t s);
 // crop [Bc][2S][64] → [Bc][T][64]
 int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16_t *dst,
               hipStream_t s);
@@ -71,9 +73,11 @@ int head_post(const HeadPostArgs &a, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---
 // ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials
-// + self-resetting counters), or null to disable tail balancing
+// + self-resetting counters), or null to disable tail balancing.
+// kmask: optional key-padding mask [B][Sk] (1 = attend), encoder semantics (attention.hip header)
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
-              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s);
+              int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s,
+              const uint8_t *kmask = nullptr);
 size_t attention_ws_bytes();
 
 // --------------------------------------------------------------- sampler ---

@@ -106,7 +106,21 @@ __global__ void cast_kernel(const float *src, bf16_t *dst, int64_t n) {
     if (i < n) dst[i] = f2bf(src[i]);
 }
 
+__global__ void copy_cols_kernel(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, int C) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)M * C) return;
+    const int64_t m = e / C, c = e - m * C;
+    dst[m * ldd + c] = src[m * lds + c];
+}
+
 }  // namespace
+
+int copy_cols(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, int C, hipStream_t s) {
+    if (M <= 0 || C <= 0) return 0;
+    copy_cols_kernel<<<(unsigned)(((int64_t)M * C + 255) / 256), 256, 0, s>>>(src, lds, dst, ldd, M, C);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
                int64_t ldy, int M, int N, int K, int act, hipStream_t s) {

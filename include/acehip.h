@@ -116,6 +116,52 @@ int acehip_dit_profile_read(acehip_dit *h, int kind, int *launches, float *total
  * bench times only the roofline kernel inside its timed region. */
 int acehip_dit_profile_kinds(acehip_dit *h, unsigned mask);
 
+/* --------------------------------------------------- condition encoders ---- */
+
+/* One stack of AceStepEncoderLayer (reference base:374-440) with its
+ * embed_tokens Linear, final Qwen3RMSNorm and optional proj_out Linear — the
+ * shape shared by AceStepLyricEncoder (base:577-731), AceStepTimbreEncoder
+ * (base:997-1178), AttentionPooler (base:734-859) and AudioTokenDetokenizer
+ * (base:862-994).  The host composes them into AceStepConditionEncoder
+ * (base:1509-1554; pack_sequences base:138-169 is index plumbing). */
+typedef struct acehip_enc_cfg {
+    int hidden;          /* 2048 */
+    int intermediate;    /* 6144 */
+    int heads;           /* 16 */
+    int kv_heads;        /* 8 */
+    int head_dim;        /* 128 */
+    int layers;          /* lyric 8, timbre 4, pooler/detokenizer 2 */
+    int window;          /* 128 (sliding layers: |i-j| <= window) */
+    int in_dim;          /* embed_tokens in-features (lyric/text 1024, timbre 64, pooler 2048) */
+    int embed_bias;      /* 1: embed_tokens has a bias */
+    int out_dim;         /* proj_out out-features (detokenizer 64), 0 = none; <= 128 */
+    float eps;           /* 1e-6 */
+    float rope_theta;    /* 1e6 */
+    int max_tokens;      /* max B*S per forward */
+    int max_S;           /* max sequence length */
+    const uint8_t *sliding; /* [layers] 1 = sliding layer; NULL = even idx */
+} acehip_enc_cfg;
+
+typedef struct acehip_enc acehip_enc;
+
+int acehip_enc_create(int device, const acehip_enc_cfg *cfg, acehip_enc **out);
+/* Names relative to the module, as in its state dict: "embed_tokens.weight",
+ * "layers.3.self_attn.q_proj.weight", "layers.3.input_layernorm.weight",
+ * "norm.weight", "proj_out.bias" ...  dtype ACEHIP_F32/BF16. */
+int acehip_enc_set_weight(acehip_enc *h, const char *name, const void *ptr, int dtype, int ndim,
+                          const int64_t *shape, int on_device);
+int acehip_enc_finalize(acehip_enc *h);
+/* embed_tokens: out bf16 [M, hidden] = x bf16 [M, in_dim] · Wᵀ (+ b)
+ * (base:623, :1085, :766, :895). */
+int acehip_enc_embed(acehip_enc *h, const void *x, int M, void *out, void *stream);
+/* layers + norm (+ proj_out): x bf16 [B, S, hidden] (not modified) →
+ * out bf16 [B, S, out_dim ? out_dim : hidden].  kmask: device uint8 [B, S]
+ * key-padding mask (1 = attend; create_4d_mask semantics, base:56-135) or
+ * NULL (no padding mask).  RoPE positions 0..S-1 per sequence. */
+int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B, int S, void *out,
+                       void *stream);
+int acehip_enc_destroy(acehip_enc *h);
+
 /* ------------------------------------------------------------ sampler ---- */
 
 /* One base/sft CFG step: cond/uncond split + APG (momentum -0.75, norm clip
@@ -205,6 +251,10 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
  * o [B,Sq,H*128]; window < 0 = full, else |i-j| <= window. */
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H,
                           int KV, int Sq, int Sk, int window, float scale, void *stream);
+/* Same with a key-padding mask kmask uint8 [B, Sk] (1 = attend), encoder semantics. */
+int acehip_attention_masked_bf16(const void *q, const void *k, const void *v, void *o, int B,
+                                 int H, int KV, int Sq, int Sk, int window, float scale,
+                                 const uint8_t *kmask, void *stream);
 
 /* Qwen3RMSNorm (+ AdaLN modulation when shift/scale are given) over rows of D
  * (transformers modeling_qwen3.py:59-64; reference base:499,530,1496):

@@ -1,0 +1,66 @@
+"""Pin the condition-encoder oracle (oracle/condenc_oracle.py) against golden
+vectors produced by the reference's own AceStepConditionEncoder
+(tools/make_golden.py gen_condenc, imported from /root/reference in the build
+container): lyric encoder with key padding (incl. rows with no admissible
+key), timbre encoder + unpack, pack_sequences, the packed encoder states."""
+import pytest
+import torch
+
+from conftest import cosine, golden_manifest, load_golden, rel_l2
+
+from acehip.config import DiTConfig
+from acehip.weights import synth_condenc_weights
+from oracle import condenc_oracle as co
+
+NAMES = ["tiny_float32", "tiny_bfloat16", "full_float32", "full_bfloat16"]
+
+
+def _setup(name):
+    meta = golden_manifest()["condenc"][name]
+    cfg = DiTConfig(**meta["cfg"])
+    g = load_golden("condenc_" + name)
+    W = synth_condenc_weights(cfg, seed=meta["seed"], mode="parity")
+    cs = float(sum(float(v.double().abs().sum()) for v in W.values()))
+    assert abs(cs - meta["weights_checksum"]) <= 1e-9 * abs(cs), "synthetic weights drifted"
+    dt = g["text"].dtype
+    return cfg, g, {k: v.to(dt) for k, v in W.items()}
+
+
+def _close(out, ref, dt):
+    if dt == torch.float32:
+        assert rel_l2(out, ref) < 1e-5
+    else:
+        assert rel_l2(out, ref) < 1e-2 and cosine(out, ref) > 0.9999
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_condition_encoder_matches_reference(name):
+    cfg, g, W = _setup(name)
+    dt = g["text"].dtype
+    with torch.no_grad():
+        lyr = co.lyric_encoder(W, cfg, g["lyric"], g["lyric_mask"])
+        tim, tmask = co.timbre_encoder(W, cfg, g["refer"], g["order"])
+        enc, mask = co.condition_encoder(W, cfg, g["text"], g["text_mask"], g["lyric"], g["lyric_mask"],
+                                         g["refer"], g["order"])
+    _close(lyr, g["lyric_out"], dt)
+    _close(tim, g["timbre_out"], dt)
+    assert torch.equal(tmask, g["timbre_mask"])
+    assert torch.equal(mask.to(torch.uint8), g["enc_mask"])
+    _close(enc, g["enc"], dt)
+
+
+def test_fully_masked_rows_are_uniform():
+    """A padded lyric query row whose band holds no valid key: the reference's
+    finite finfo.min mask makes its softmax uniform over ALL keys — the HIP
+    kernel's masked mode reproduces exactly this (attention.hip header)."""
+    S, W_ = 40, 4
+    m = torch.ones(1, S, dtype=torch.long)
+    m[0, 10:] = 0
+    mask = co.create_4d_mask(S, torch.float32, m, W_)
+    row = mask[0, 0, 30]          # |30 − j| ≤ 4 → j ∈ [26, 34], all padding
+    assert bool((row == torch.finfo(torch.float32).min).all())
+    q = torch.randn(1, 1, S, 128)
+    k = torch.randn(1, 1, S, 128)
+    v = torch.randn(1, 1, S, 128)
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+    assert torch.allclose(o[0, 0, 30], v[0, 0].mean(0), atol=1e-5)

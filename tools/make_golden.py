@@ -202,6 +202,58 @@ def gen_adg_direct(name, B, T, seed, sigmas, guidance):
     return {"B": B, "T": T, "sigmas": sigmas, "guidance": guidance}
 
 
+def condenc_config(width: str) -> DiTConfig:
+    if width == "tiny":
+        return DiTConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=4, num_attention_heads=2,
+                         num_key_value_heads=1, head_dim=128, sliding_window=8,
+                         num_lyric_encoder_hidden_layers=3, num_timbre_encoder_hidden_layers=2,
+                         num_attention_pooler_hidden_layers=2)
+    return DiTConfig(num_hidden_layers=2, num_lyric_encoder_hidden_layers=2, num_timbre_encoder_hidden_layers=1,
+                     num_attention_pooler_hidden_layers=1)
+
+
+def gen_condenc(name, width, dtype, seed):
+    """AceStepConditionEncoder.forward (base:1527-1554) on ragged padded inputs:
+    lyric rows with padding (and, with the 8-wide band of the tiny config, padded
+    query rows that see NO admissible key — the uniform-softmax case), text rows
+    with padding, 3 packed timbre references for 2 songs (order [0, 1, 1])."""
+    from acehip.weights import synth_condenc_weights
+    C, M = _import_ref("base")
+    cfg = condenc_config(width)
+    rc = ref_config(C, cfg, num_lyric_encoder_hidden_layers=cfg.num_lyric_encoder_hidden_layers,
+                    num_timbre_encoder_hidden_layers=cfg.num_timbre_encoder_hidden_layers,
+                    num_attention_pooler_hidden_layers=cfg.num_attention_pooler_hidden_layers)
+    model = M.AceStepConditionEncoder(rc).eval()
+    W = synth_condenc_weights(cfg, seed=seed, mode="parity")
+    missing, unexpected = model.load_state_dict(W, strict=False)
+    assert not unexpected and all("rotary" in k for k in missing), (missing, unexpected)
+    model = model.to(dtype)
+    g = torch.Generator().manual_seed(seed + 1)
+    B, Lt, Ll, Nref, Tref = 2, 7, 41, 3, 30
+    text = torch.randn(B, Lt, cfg.text_hidden_dim, generator=g).to(dtype)
+    tmask = torch.ones(B, Lt, dtype=torch.long)
+    tmask[1, 4:] = 0
+    lyric = torch.randn(B, Ll, cfg.text_hidden_dim, generator=g).to(dtype)
+    lmask = torch.ones(B, Ll, dtype=torch.long)
+    lmask[1, 17:] = 0
+    lmask[0, 39:] = 0
+    refer = torch.randn(Nref, Tref, cfg.timbre_hidden_dim, generator=g).to(dtype)
+    order = torch.tensor([0, 1, 1], dtype=torch.long)
+    with torch.no_grad():
+        lyr = model.lyric_encoder(inputs_embeds=lyric, attention_mask=lmask).last_hidden_state
+        tim, tim_mask = model.timbre_encoder(refer, order)
+        enc, enc_mask = model(text_hidden_states=text, text_attention_mask=tmask, lyric_hidden_states=lyric,
+                              lyric_attention_mask=lmask, refer_audio_acoustic_hidden_states_packed=refer,
+                              refer_audio_order_mask=order)
+    save_file({"text": text, "text_mask": tmask, "lyric": lyric, "lyric_mask": lmask, "refer": refer,
+               "order": order, "lyric_out": lyr.contiguous(), "timbre_out": tim.contiguous(),
+               "timbre_mask": tim_mask.contiguous(), "enc": enc.contiguous(),
+               "enc_mask": enc_mask.to(torch.uint8).contiguous()},
+              os.path.join(OUT, f"condenc_{name}.safetensors"))
+    return {"width": width, "cfg": cfg.__dict__, "dtype": str(dtype), "seed": seed,
+            "weights_checksum": checksum(W)}
+
+
 def main_only(which):
     """Add fixtures to an existing manifest without regenerating the rest."""
     torch.set_num_threads(8)
@@ -214,6 +266,13 @@ def main_only(which):
         manifest["sampler"]["base_s8_adg"] = gen_sampler("base", "base_s8_adg", bf, 1, 40, infer_steps=8,
                                                          shift=3.0, diffusion_guidance_sale=7.0,
                                                          use_adg=True)
+    if "condenc" in which:
+        ce = {}
+        for width in ("tiny", "full"):
+            for dt in (torch.float32, torch.bfloat16):
+                tag = f"{width}_{str(dt).split('.')[-1]}"
+                ce[tag] = gen_condenc(tag, width, dt, 31 if width == "tiny" else 32)
+        manifest["condenc"] = ce
     with open(mpath, "w") as f:
         json.dump(manifest, f, indent=1, default=str)
     print("updated", mpath)
