@@ -49,6 +49,10 @@ def parse():
     p.add_argument("--lenc", type=int, default=641)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-vae", action="store_true")
+    p.add_argument("--no-condition", action="store_true",
+                   help="feed synthetic encoder states directly (skip the HIP condition encoders)")
+    p.add_argument("--lyric-len", type=int, default=512)
+    p.add_argument("--text-len", type=int, default=128)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -91,7 +95,8 @@ def main():
     from acehip.config import DiTConfig, VAEConfig
     from acehip.dit import AceStepDiTBackend, DiTRuntime
     from acehip.vae import OobleckBackend
-    from acehip.weights import synth_dit_weights, synth_null_condition, synth_vae_weights
+    from acehip.weights import synth_condenc_weights, synth_dit_weights, synth_null_condition, synth_vae_weights
+    from acehip.condition import ConditionEncoder, HipPrepareCondition
     from acehip.flops import dit_flops_per_row, vae_decoder_flops
 
     rank, world, local = D.env_world()
@@ -111,7 +116,14 @@ def main():
     null = synth_null_condition(cfg, seed=0, device=dev, dtype=torch.bfloat16, backend="torch")
     rt = DiTRuntime(cfg, local, max_S=S, max_Bc=Bc, max_Lenc=args.lenc)
     rt.load(W)
-    be = AceStepDiTBackend(rt, null, is_turbo=False)
+    prep = None
+    if not args.no_condition:
+        # lyric + timbre + text encoders on the HIP path; Lenc = lyric + 1 timbre + text
+        ce = ConditionEncoder(cfg, local, max_batch=1, max_lyric=args.lyric_len, max_refs=1, max_ref_frames=750)
+        ce.load(synth_condenc_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch"))
+        prep = HipPrepareCondition(ce)
+        args.lenc = args.lyric_len + 1 + args.text_len
+    be = AceStepDiTBackend(rt, null, is_turbo=False, prepare_condition=prep)
     vae = vae_w = None
     if not args.no_vae:
         vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=False, device=dev,
@@ -121,10 +133,26 @@ def main():
 
     # synthetic conditioning on rank 0, broadcast over RCCL
     g = torch.Generator(device=dev).manual_seed(1234)
-    enc = torch.randn(1, args.lenc, cfg.hidden_size, device=dev, generator=g).bfloat16()
-    ctx = torch.cat([torch.randn(1, T, 64, device=dev, generator=g),
-                     torch.ones(1, T, 64, device=dev)], dim=-1).bfloat16().contiguous()
-    D.broadcast_condition([enc, ctx])
+    src = torch.randn(1, T, 64, device=dev, generator=g).bfloat16()          # silence latents
+    chunk = torch.ones(1, T, 64, device=dev).bfloat16()
+    if args.no_condition:
+        enc = torch.randn(1, args.lenc, cfg.hidden_size, device=dev, generator=g).bfloat16()
+        ctx = torch.cat([src, chunk], dim=-1).contiguous()
+        D.broadcast_condition([enc, ctx])
+        cond_kw = dict(encoder_hidden_states=enc, context_latents=ctx)
+    else:
+        # text-encoder / lyric-embedding outputs and a 30 s timbre reference (the inputs of
+        # prepare_condition, base:1607-1652); the encoders run inside the timed song
+        text = torch.randn(1, args.text_len, cfg.text_hidden_dim, device=dev, generator=g).bfloat16()
+        lyric = torch.randn(1, args.lyric_len, cfg.text_hidden_dim, device=dev, generator=g).bfloat16()
+        refer = torch.randn(1, 750, cfg.timbre_hidden_dim, device=dev, generator=g).bfloat16()
+        D.broadcast_condition([text, lyric, refer, src])
+        cond_kw = dict(text_hidden_states=text, text_attention_mask=torch.ones(1, args.text_len, device=dev, dtype=torch.long),
+                       lyric_hidden_states=lyric,
+                       lyric_attention_mask=torch.ones(1, args.lyric_len, device=dev, dtype=torch.long),
+                       refer_audio_acoustic_hidden_states_packed=refer,
+                       refer_audio_order_mask=torch.zeros(1, device=dev, dtype=torch.long),
+                       src_latents=src, chunk_masks=chunk, is_covers=torch.zeros(1, device=dev, dtype=torch.long))
 
     dit_s_total = [0.0]
     vae_s_total = [0.0]
@@ -134,8 +162,7 @@ def main():
         e1 = torch.cuda.Event(enable_timing=True)
         e2 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        res = be.generate_audio(encoder_hidden_states=enc, context_latents=ctx,
-                                infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance,
+        res = be.generate_audio(**cond_kw, infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance,
                                 shift=args.shift, seed=seed, infer_method="ode")
         e1.record()
         if vae is not None:
@@ -199,11 +226,13 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (random-init weights of the real architecture, random conditioning)",
         "config": {"workload": f"text2music {args.seconds:g}s, base/sft {args.infer_steps} steps, "
-                               f"shift {args.shift:g}, CFG {args.guidance:g} + APG, DiT + VAE decode",
+                               f"shift {args.shift:g}, CFG {args.guidance:g} + APG, "
+                               + ("DiT + VAE decode" if args.no_condition else "condition encoders + DiT + VAE decode"),
                    "global_batch": songs, "seq_len": S, "latent_frames": T, "lenc": args.lenc,
                    "parallelism": f"song-parallel x{world}"},
         "songs_per_s": round(songs / elapsed_max, 4),
         "dit_ms_per_song": round(dit_ms, 2),
+        "dit_ms_note": "generate_audio wall on the GPU stream: condition encoders (once) + 27 CFG DiT steps",
         "dit_ms_per_step": round(dit_ms / args.infer_steps, 3),
         "vae_ms_per_song": round(vae_ms, 2),
         "dit_tflops": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
