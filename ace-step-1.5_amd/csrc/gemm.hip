@@ -32,6 +32,9 @@ namespace {
 
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
+#ifndef PP_SCHED
+#define PP_SCHED -1        // ping-pong main loop: -1 per tile (256 rows: 1, 192 rows: 0); 0 12/4/8/0-read phases, 1 8/4/8/4, 2 two phases
+#endif
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
@@ -298,6 +301,124 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 
     const int fr = lane & 15, fc = lane >> 4;
     const int arow = wr * TM, brow = BM + wc * 64;
+
+    const int nk = a.K / BK;
+    // prologue: tile 0 complete, B(1) in flight
+    stageB(0, 0);
+    stageA(0, 0);
+    if (nk > 1) {
+        stageB(1, BK);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    if (wr == 1) bar();   // group 1 runs one barrier behind
+
+    constexpr int SCHED = PP_SCHED >= 0 ? PP_SCHED : (BM == 256 ? 1 : 0);
+    if constexpr (SCHED == 2) {
+    // Two phases per K-tile (k-step 0, k-step 1; 32 MFMAs each): half the barriers of
+    // the 4-phase schedules.  Phase 0 stages the whole next tile (A and B) into the
+    // other buffer, whose last reads (the partner group's phase 1 of tile kt−1)
+    // completed before this window's opening barrier; phase 1 waits for its own DMAs.
+    bf16x8 xk[2 * SMH], bk[4];
+    auto readA2 = [&](const char *b, int ks) {
+#pragma unroll
+        for (int i = 0; i < 2 * SMH; ++i) xk[i] = *(const bf16x8 *)(b + swz(arow + i * 16 + fr, ks * 4 + fc));
+    };
+    auto readB2 = [&](const char *b, int ks) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bk[j] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
+    };
+    auto mma2 = [&] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2 * SMH; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bk[j], xk[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+        const char *b = lds + (kt & 1) * BUF;
+        readB2(b, 0);
+        readA2(b, 0);
+        if (kt + 1 < nk) {
+            stageA((kt + 1) & 1, (kt + 1) * BK);
+            if (kt >= 1) stageB((kt + 1) & 1, (kt + 1) * BK);   // B(1) came with the prologue
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        mma2();
+        bar();
+        readB2(b, 1);
+        readA2(b, 1);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        bar();
+        mma2();
+        bar();
+    }
+    } else if constexpr (SCHED == 1) {
+    // Balanced schedule: phase p multiplies A-half (p & 1) by all four B sub-tiles at
+    // k-step (p >> 1), so a loader wave issues 8, 4, 8, 4 ds_read_b128 per phase (the
+    // 12-read first phase of the schedule below, plus the A(kt+1) DMA, saturates the
+    // 256 B/clk LDS array against a 256-cycle MFMA phase) and holds 8 operand
+    // fragments instead of 16.  Reads complete (lgkmcnt(0)) BEFORE each barrier, so
+    // the WAR margins of the DMAs (A(kt+1) after tile kt−1's phase-3 reads, B(kt+2)
+    // after tile kt's phase-2 reads) are one barrier each.
+    bf16x8 xk[SMH], bk[4];
+    auto readA1 = [&](const char *b, int h, int ks) {
+#pragma unroll
+        for (int i = 0; i < SMH; ++i) xk[i] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
+    };
+    auto readB1 = [&](const char *b, int ks) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bk[j] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
+    };
+    auto mma1 = [&](int h) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < SMH; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[h * SMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bk[j], xk[i], acc[h * SMH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    for (int kt = 0; kt < nk; ++kt) {
+        const char *b = lds + (kt & 1) * BUF;
+        readB1(b, 0);
+        readA1(b, 0, 0);
+        if (kt + 1 < nk) stageA((kt + 1) & 1, (kt + 1) * BK);
+        lgkm0();
+        bar();
+        mma1(0);
+        bar();
+        readA1(b, 1, 0);
+        lgkm0();
+        bar();
+        mma1(1);
+        bar();
+        readB1(b, 1);
+        readA1(b, 0, 1);
+        lgkm0();
+        bar();
+        mma1(0);
+        bar();
+        readA1(b, 1, 1);
+        if (kt + 2 < nk) {
+            stageB(kt & 1, (kt + 2) * BK);
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        bar();
+        mma1(1);
+        bar();
+    }
+    } else {
     bf16x8 xa[SMH][2], b0[2][2], b1[2][2];
     auto readA = [&](const char *b, int h) {
 #pragma unroll
@@ -327,20 +448,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[j][ks], xa[i][ks], acc[h * SMH + i][q * 2 + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
-
-    const int nk = a.K / BK;
-    // prologue: tile 0 complete, B(1) in flight
-    stageB(0, 0);
-    stageA(0, 0);
-    if (nk > 1) {
-        stageB(1, BK);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    bar();
-    if (wr == 1) bar();   // group 1 runs one barrier behind
-
     for (int kt = 0; kt < nk; ++kt) {
         const char *b = lds + (kt & 1) * BUF;
         // phase 0
@@ -370,6 +477,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         bar();
         mma(1, 0, b0);
         bar();
+    }
     }
     if (wr == 0) bar();   // balance the barrier count
 

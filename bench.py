@@ -52,6 +52,11 @@ def parse():
     p.add_argument("--no-condition", action="store_true",
                    help="feed synthetic encoder states directly (skip the HIP condition encoders)")
     p.add_argument("--lyric-len", type=int, default=512)
+    p.add_argument("--repaint", action="store_true",
+                   help="SURVEY config 5: VAE encode of a synthetic 48 kHz stereo source -> DiT repaint of "
+                        "[--repaint-start, --repaint-end) s -> VAE decode, all inside the timed song")
+    p.add_argument("--repaint-start", type=float, default=60.0)
+    p.add_argument("--repaint-end", type=float, default=120.0)
     p.add_argument("--text-len", type=int, default=128)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
@@ -126,9 +131,9 @@ def main():
     be = AceStepDiTBackend(rt, null, is_turbo=False, prepare_condition=prep)
     vae = vae_w = None
     if not args.no_vae:
-        vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=False, device=dev,
+        vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=args.repaint, device=dev,
                                   dtype=torch.bfloat16, backend="torch")
-        vae = OobleckBackend(vcfg, local, max_T=T, with_encoder=False)
+        vae = OobleckBackend(vcfg, local, max_T=T, with_encoder=args.repaint)
         vae.load(vae_w)
 
     # synthetic conditioning on rank 0, broadcast over RCCL
@@ -154,6 +159,23 @@ def main():
                        refer_audio_order_mask=torch.zeros(1, device=dev, dtype=torch.long),
                        src_latents=src, chunk_masks=chunk, is_covers=torch.zeros(1, device=dev, dtype=torch.long))
 
+    span = None
+    if args.repaint:
+        assert vae is not None and not args.no_condition, "--repaint needs the VAE and the condition encoders"
+        # synthetic source: 3 seeded sines + N(0, 0.05), peak −12 dBFS
+        n = T * vcfg.hop_length
+        tt = torch.arange(n, device=dev, dtype=torch.float32) / 48000.0
+        sw = sum(torch.sin(2 * math.pi * f * tt + ph) for f, ph in ((220.0, 0.1), (330.0, 0.7), (523.25, 1.9)))
+        sw = torch.stack([sw, torch.roll(sw, 480)])[None]
+        sw = sw + 0.05 * torch.randn(sw.shape, device=dev, generator=g)
+        src_wav = (sw / sw.abs().amax() * 10 ** (-12 / 20)).bfloat16().contiguous()
+        del sw, tt
+        D.broadcast_condition([src_wav])
+        # conditioning_masks.py:37-50: latent span [start·48000//1920, end·48000//1920)
+        span = (int(args.repaint_start * 48000 // 1920), int(args.repaint_end * 48000 // 1920))
+        span_mask = torch.zeros(1, T, 64, device=dev, dtype=torch.bfloat16)
+        span_mask[:, span[0]:span[1]] = 1
+
     dit_s_total = [0.0]
     vae_s_total = [0.0]
 
@@ -162,6 +184,14 @@ def main():
         e1 = torch.cuda.Event(enable_timing=True)
         e2 = torch.cuda.Event(enable_timing=True)
         e0.record()
+        if span is not None:
+            # vae.encode(x).latent_dist.sample() (vae_encode.py:65), then the repaint source:
+            # encoded target with silence inside the span + chunk mask of the span
+            # (conditioning_masks.py:67-83)
+            z = vae.encode_tensor(src_wav, sample=True).transpose(1, 2)
+            src_r = z.clone()
+            src_r[:, span[0]:span[1]] = src[:, span[0]:span[1]]
+            cond_kw.update(src_latents=src_r.contiguous(), chunk_masks=span_mask)
         res = be.generate_audio(**cond_kw, infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance,
                                 shift=args.shift, seed=seed, infer_method="ode")
         e1.record()
@@ -213,7 +243,7 @@ def main():
     kernels = {k: {"launches": n, "avg_us": (ms / n * 1e3 if n else None)} for k, (n, ms) in prof_all.items()}
 
     out = {
-        "metric": "seconds/song (240 s audio, 27 DiT steps)",
+        "metric": f"seconds/song ({args.seconds:g} s audio, {args.infer_steps} DiT steps)",
         "value": round(sec_per_song, 4),
         "unit": "s/song",
         "n_gpus": world,
@@ -227,12 +257,14 @@ def main():
         "data": "synthetic (random-init weights of the real architecture, random conditioning)",
         "config": {"workload": f"text2music {args.seconds:g}s, base/sft {args.infer_steps} steps, "
                                f"shift {args.shift:g}, CFG {args.guidance:g} + APG, "
-                               + ("DiT + VAE decode" if args.no_condition else "condition encoders + DiT + VAE decode"),
+                               + ("DiT + VAE decode" if args.no_condition else "condition encoders + DiT + VAE decode")
+                               + (f", repaint [{args.repaint_start:g}, {args.repaint_end:g}) s: VAE encode first"
+                                  if args.repaint else ""),
                    "global_batch": songs, "seq_len": S, "latent_frames": T, "lenc": args.lenc,
                    "parallelism": f"song-parallel x{world}"},
         "songs_per_s": round(songs / elapsed_max, 4),
         "dit_ms_per_song": round(dit_ms, 2),
-        "dit_ms_note": "generate_audio wall on the GPU stream: condition encoders (once) + 27 CFG DiT steps",
+        "dit_ms_note": "generate_audio wall on the GPU stream: (repaint: VAE encode +) condition encoders (once) + CFG DiT steps",
         "dit_ms_per_step": round(dit_ms / args.infer_steps, 3),
         "vae_ms_per_song": round(vae_ms, 2),
         "dit_tflops": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
