@@ -105,6 +105,11 @@ class DiTRuntime:
         self._enc_keepalive = enc
         self.Bc, self.Lenc = Bc, Lenc
 
+    def set_uniform_rows(self, first_row: int):
+        """Rows [first_row, Bc) of the condition are one vector repeated (CFG null rows):
+        their cross-attention is computed in closed form (acehip_dit_set_uniform_rows)."""
+        check(lib().acehip_dit_set_uniform_rows(self.h, int(first_row), stream_ptr()), "set_uniform_rows")
+
     def forward(self, xt: torch.Tensor, ctx: torch.Tensor, t: torch.Tensor,
                 t_r: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One decoder forward.  xt [Bx,T,64], ctx [Bx,T,128] bf16; t/t_r: fp32
@@ -230,6 +235,7 @@ class AceStepDiTBackend:
         self.null = null_condition_emb.detach().to(self.device, dtype)
         self.is_turbo = is_turbo
         self.prepare_condition = prepare_condition
+        self.uniform_null = True     # closed-form cross-attention for the CFG null rows
 
     @classmethod
     def from_reference_model(cls, model, max_seconds: float = 600.0, max_batch: int = 8,
@@ -315,7 +321,13 @@ class AceStepDiTBackend:
 
     def _set_cond(self, enc, cfg):
         if cfg:
-            enc = torch.cat([enc, self.null.expand_as(enc)], dim=0)
+            B = enc.shape[0]
+            enc = torch.cat([enc, self.null.expand_as(enc)], dim=0)     # base:1907
+            self.rt.set_condition(enc)
+            # the null rows repeat one vector: closed-form cross-attention for them
+            if self.uniform_null and self.null.numel() == enc.shape[-1]:
+                self.rt.set_uniform_rows(B)
+            return
         self.rt.set_condition(enc)
 
     def _base_loop(self, kw, enc, ctx, enc_nc, ctx_nc, acs):

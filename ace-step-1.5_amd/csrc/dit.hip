@@ -67,6 +67,11 @@ struct acehip_dit {
     bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
+    // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
+    // encoder sequence that is one vector repeated, so their cross-attention is the
+    // constant V row and their cross-O output the per-layer constant cnull[l]
+    int uniform_from = 1 << 30;
+    bf16_t *cnull = nullptr, *vnull = nullptr;   // [L][D], [q_dim]
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
     size_t tmp_elems = 0;
 
@@ -248,6 +253,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->mod = A((size_t)L * Bc * 6 * D); h->mod_out = A(Bc * 2 * D);
     h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd);
+    h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
     h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
     h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
@@ -430,6 +436,32 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
     h->have_cond = true;
     h->cond_Bc = Bc;
     h->cond_Lenc = Lenc;
+    h->uniform_from = 1 << 30;
+    return 0;
+}
+
+int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    if (!h->have_cond) return fail(ACEHIP_E_STATE, "set_uniform_rows before set_condition");
+    if (first_row <= 0 || first_row > h->cond_Bc) return fail(ACEHIP_E_ARG, "set_uniform_rows: first_row in [1, Bc]");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    h->uniform_from = 1 << 30;
+    if (first_row == h->cond_Bc) return 0;   // none uniform
+    const int D = h->D, qd = h->qd, kvd = h->kvd, Le = h->cond_Lenc;
+    const size_t per = (size_t)h->cond_Bc * kvd * Le;
+    for (int l = 0; l < h->L; ++l) {
+        // softmax over identical keys is uniform: every query's output is V row 0 of its
+        // KV head (bit-exact: Σ of Lenc equal terms and the division are exact in fp32)
+        int rc = gather_head_row(h->Vc + l * per + (size_t)first_row * kvd * Le, h->cfg.kv_heads, Le, h->cfg.heads,
+                                 h->vnull, s);
+        if (rc) return rc;
+        GemmArgs g{};
+        g.A = h->vnull; g.lda = qd; g.W = h->layers[l].wco; g.ldw = qd; g.C = h->cnull + (size_t)l * D; g.ldc = D;
+        g.M = 1; g.N = D; g.K = qd; g.epi = EPI_STORE;
+        if ((rc = gemm(g, s))) return rc;
+    }
+    h->uniform_from = first_row;
     return 0;
 }
 
@@ -467,6 +499,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     RUN(gemm(g, s));
 
     const size_t cper = (size_t)Bc * kvd * Le;
+    const int Bq = std::min(h->uniform_from, Bc), Mq = Bq * S;   // rows with a real cross-attention
     for (int l = 0; l < L; ++l) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
@@ -490,22 +523,24 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
         RUN(timed(h, 3, s, [&] { return gemm(o, s); }));
-        // --- cross-attention, plain residual (base:513-526)
-        RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
+        // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
+        // rows, base:1907) get their constant cross-O output cnull[l] (set_uniform_rows)
+        RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, Mq, D, eps, s));
         GemmArgs cq{};
         cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D;
-        cq.M = M; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
-        cq.hp.B = Bc; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
+        cq.M = Mq; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
+        cq.hp.B = Bq; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
         cq.hp.eps = eps;
         RUN(gemm(cq, s));
         RUN(timed(h, 6, s, [&] {
-            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bc, H, KV, S, Le, -1, scale, qd,
+            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bq, H, KV, S, Le, -1, scale, qd,
                              h->attn_ws, s);
         }));
         GemmArgs co{};
         co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
-        co.M = M; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
+        co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
         RUN(timed(h, 3, s, [&] { return gemm(co, s); }));
+        if (Mq < M) RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533)
         RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s));
         GemmArgs gu{};

@@ -55,6 +55,10 @@ int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj,
 // proj_in input pack: X[b][s][k*192+c] = (c<128 ? ctx : xt)[b % Bx][2s+k][..] or 0
 int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
                  hipStream_t s);
+// out[h·128 + d] = V[h / (H/KV)][0][d]  (row 0 of each KV head, V [KV][Le][128])
+int gather_head_row(const bf16_t *V, int KV, int Le, int H, bf16_t *out, hipStream_t s);
+// X[r][:] = bf16(X[r][:] + c[:]) for rows r < rows (c bf16 [D])
+int add_row_bcast(bf16_t *X, const bf16_t *c, int rows, int D, hipStream_t s);
 // dst[m][0:C] = src[m][0:C] (row-strided column block copy)
 int copy_cols(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, int C, hipStream_t s);
 // crop [Bc][2S][64] → [Bc][T][64]

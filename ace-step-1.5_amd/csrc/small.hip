@@ -113,7 +113,41 @@ __global__ void copy_cols_kernel(const bf16_t *src, int64_t lds, bf16_t *dst, in
     dst[m * ldd + c] = src[m * lds + c];
 }
 
+__global__ void gather_head_row_kernel(const bf16_t *V, int KV, int Le, int H, bf16_t *out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;   // e = h·128 + d
+    if (e >= H * 128) return;
+    const int h = e >> 7, d = e & 127;
+    out[e] = V[((int64_t)(h / (H / KV)) * Le) * 128 + d];
+}
+
+__global__ void add_row_bcast_kernel(bf16_t *X, const bf16_t *c, int64_t n8, int D8) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    float x[8], y[8];
+    unpack8(((const uint4 *)X)[i], x);
+    unpack8(((const uint4 *)c)[i % D8], y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += y[j];
+    ((uint4 *)X)[i] = pack8(x);
+}
+
 }  // namespace
+
+int gather_head_row(const bf16_t *V, int KV, int Le, int H, bf16_t *out, hipStream_t s) {
+    if (KV <= 0 || H % KV) return fail(-1, "gather_head_row: heads");
+    gather_head_row_kernel<<<(H * 128 + 255) / 256, 256, 0, s>>>(V, KV, Le, H, out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int add_row_bcast(bf16_t *X, const bf16_t *c, int rows, int D, hipStream_t s) {
+    if (rows <= 0) return 0;
+    if (D % 8) return fail(-1, "add_row_bcast: D % 8");
+    const int64_t n8 = (int64_t)rows * D / 8;
+    add_row_bcast_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(X, c, n8, D / 8);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int copy_cols(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, int C, hipStream_t s) {
     if (M <= 0 || C <= 0) return 0;

@@ -92,6 +92,16 @@ int acehip_dit_finalize(acehip_dit *h);
  * enc: bf16 [Bc, Lenc, hidden] (CFG: cond rows then null rows). */
 int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, void *stream);
 
+/* Declare batch rows [first_row, Bc) of the current condition uniform: their
+ * encoder sequence is ONE vector repeated (the CFG null rows,
+ * null_condition_emb.expand_as, base:1907).  The decoder never masks encoder
+ * positions (base:1384-1385), so such a row's cross-attention softmax is
+ * exactly uniform and its output is V row 0 for every query; forward then
+ * skips the cross-Q projection / attention / cross-O GEMM for those rows and
+ * adds the per-layer constant cross-O output (precomputed here).  first_row ==
+ * Bc turns it off; set_condition resets it. */
+int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream);
+
 /* One decoder forward: AceStepDiTModel.forward
  * (acestep/models/base/modeling_acestep_v15_base.py:1303-1507).
  * xt: bf16 [Bx, T, 64]; ctx: bf16 [Bx, T, 128]; batch row b of the DiT reads

@@ -341,3 +341,33 @@ def test_turbo_generate_audio_runs(gpu_device):
     x = res["target_latents"]
     assert x.shape == (1, 40, 64) and torch.isfinite(x.float()).all()
     rt.close()
+
+
+def test_uniform_null_rows_closed_form(gpu_device):
+    """CFG null rows (null_condition_emb repeated, base:1907): the closed-form cross-attention
+    (acehip_dit_set_uniform_rows) equals the full computation of those rows."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=4, window=8)
+    W = synth_dit_weights(cfg, seed=3, mode="parity")
+    rt = DiTRuntime(cfg, 0, max_S=64, max_Bc=4, max_Lenc=40)
+    rt.load({k: v.to(gpu_device, torch.bfloat16) for k, v in W.items()})
+    g = torch.Generator().manual_seed(5)
+    B, T, Le = 2, 100, 37
+    xt = torch.randn(B, T, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(B, T, 128, generator=g).bfloat16().to(gpu_device)
+    enc = torch.randn(B, Le, cfg.hidden_size, generator=g).bfloat16()
+    null = torch.randn(1, 1, cfg.hidden_size, generator=g).bfloat16()
+    encc = torch.cat([enc, null.expand_as(enc)]).to(gpu_device)
+    t = torch.tensor([0.625], dtype=torch.float32, device=gpu_device)
+    rt.set_condition(encc)
+    full = rt.forward(xt, ctx, t).float().clone()
+    rt.set_uniform_rows(B)
+    fast = rt.forward(xt, ctx, t).float()
+    torch.cuda.synchronize()
+    assert torch.equal(fast[:B], full[:B])                      # conditional rows untouched
+    assert rel_l2(fast[B:].cpu(), full[B:].cpu()) < 2e-3          # closed form vs full (bf16 rounding)
+    rt.set_uniform_rows(2 * B)                                    # off again
+    again = rt.forward(xt, ctx, t).float()
+    torch.cuda.synchronize()
+    assert torch.equal(again, full)
+    rt.close()
