@@ -13,6 +13,17 @@ Seams:
              and ``handler.vae.encode(x).latent_dist.sample()``
              (``vae_encode.py:65``): replaced by :class:`~acehip.vae.OobleckBackend`.
 
+  * cond   — ``prepare_condition`` (``base:1607-1652``, called from
+             ``generate_audio`` ``base:1820``): replaced by
+             :class:`~acehip.condition.HipPrepareCondition` (text projector, lyric
+             and timbre encoders on libacehip); cover conditioning that needs the
+             FSQ audio tokenizer goes to the reference's own ``prepare_condition``.
+  * LoRA   — ``add_lora`` / ``remove_lora`` / ``unload_lora`` / ``set_lora_scale`` /
+             ``set_use_lora`` / ``set_active_lora_adapter`` (``handler/lora/lifecycle.py:164-420``,
+             ``lora/controls.py:12-157``) change the decoder's effective weights;
+             :func:`install` wraps them so the merged weights are re-packed into the
+             handle afterwards (:func:`refresh_decoder_weights`).
+
 Failure policy: by default an acehip error propagates (the request fails
 loudly, ``generate_music.py:181-190`` turns it into an error payload).  The
 MLX precedent instead logs and falls back to the PyTorch path
@@ -24,6 +35,9 @@ from __future__ import annotations
 import logging
 from typing import Optional
 
+import torch
+
+from .condition import ConditionEncoder, HipPrepareCondition
 from .config import VAEConfig
 from .dit import AceStepDiTBackend
 from .vae import OobleckBackend
@@ -46,11 +60,62 @@ def vae_from_diffusers(vae, max_seconds: float = 600.0, with_encoder: bool = Tru
     return be
 
 
+def merged_decoder_state_dict(decoder) -> dict:
+    """Effective (adapter-merged) decoder weights under the plain HF names.
+
+    Works on a bare ``AceStepDiTModel`` and on a PEFT-wrapped one (``PeftModel``
+    / LoRA layers with ``base_layer`` + ``get_delta_weight``, as created by
+    ``lifecycle.py:249-258``; LyCORIS LoKr modules expose the same two): every
+    adapted Linear becomes ``base.weight + Σ_active get_delta_weight(a)`` unless
+    the adapters are disabled or already merged; PEFT's name decorations
+    (``base_model.model.``, ``.base_layer``) are stripped."""
+    out = {}
+    with torch.no_grad():
+        for name, mod in decoder.named_modules():
+            base = getattr(mod, "base_layer", None)
+            if base is None or not hasattr(mod, "get_delta_weight"):
+                continue
+            w = base.weight.detach().float().clone()
+            if not getattr(mod, "disable_adapters", False) and not getattr(mod, "merged", False):
+                act = getattr(mod, "active_adapters", None) or []
+                for a in ([act] if isinstance(act, str) else act):
+                    try:
+                        w += mod.get_delta_weight(a).float()
+                    except KeyError:      # adapter not present on this layer
+                        pass
+            out[name + ".weight"] = w
+            if getattr(base, "bias", None) is not None:
+                out[name + ".bias"] = base.bias.detach()
+        for k, v in decoder.state_dict().items():
+            if ".base_layer." in k or "lora_" in k or "lokr_" in k or ".hada_" in k:
+                continue
+            out.setdefault(k, v)
+    clean = {}
+    for k, v in out.items():
+        if k.startswith("base_model.model."):
+            k = k[len("base_model.model."):]
+        clean[k.replace(".base_layer", "")] = v
+    return clean
+
+
+def refresh_decoder_weights(dit: AceStepDiTBackend, decoder) -> None:
+    """Re-pack the decoder's current effective weights into the DiT handle
+    (§8f row 3: LoRA add/remove/scale changes)."""
+    dit.rt.load(merged_decoder_state_dict(decoder))
+
+
+_LORA_METHODS = ("add_lora", "load_lora", "add_voice_lora", "remove_lora", "unload_lora", "set_lora_scale",
+                 "set_use_lora", "set_active_lora_adapter")
+
+
 def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: bool = False,
-            vae: bool = True) -> dict:
+            vae: bool = True, condition: bool = True) -> dict:
     """Swap the handler's DiT sampler and VAE for the acehip backends."""
     dit = AceStepDiTBackend.from_reference_model(handler.model, max_seconds=max_seconds,
                                                  max_batch=max_batch)
+    if condition:
+        ce = ConditionEncoder.from_reference_model(handler.model, max_batch=max_batch)
+        dit.prepare_condition = HipPrepareCondition(ce, fallback=handler.model.prepare_condition)
     orig_generate = handler.model.generate_audio
 
     def generate_audio(**kw):
@@ -64,6 +129,18 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
 
     handler.model.generate_audio = generate_audio
     out = {"dit": dit}
+
+    # LoRA lifecycle: after any adapter change re-pack the merged decoder weights
+    for meth in _LORA_METHODS:
+        orig = getattr(handler, meth, None)
+        if orig is None:
+            continue
+
+        def wrapped(*a, _orig=orig, **k):
+            res = _orig(*a, **k)
+            refresh_decoder_weights(dit, handler.model.decoder)
+            return res
+        setattr(handler, meth, wrapped)
     if vae and getattr(handler, "vae", None) is not None:
         vb = vae_from_diffusers(handler.vae, max_seconds=max_seconds)
         orig_decode, orig_encode = handler.vae.decode, handler.vae.encode

@@ -106,3 +106,48 @@ def test_gloo_world2_broadcast_and_max():
     for rank, es, cs, m, g in res:
         assert es == sum(range(40)) and cs == 84.0 and m == 10.0
     assert res[0][4] == [0, 1]
+
+
+def test_lora_merge_state_dict():
+    """§8f row 3: the LoRA re-pack hook merges PEFT-style adapted Linears
+    (base_layer + get_delta_weight over the active adapters) into plain HF names."""
+    import torch
+    from acehip.integration import merged_decoder_state_dict
+
+    class LoraLinear(torch.nn.Module):
+        def __init__(self, base, r=2, scale=0.5):
+            super().__init__()
+            self.base_layer = base
+            self.lora_A = torch.nn.ModuleDict({"v": torch.nn.Linear(base.in_features, r, bias=False)})
+            self.lora_B = torch.nn.ModuleDict({"v": torch.nn.Linear(r, base.out_features, bias=False)})
+            self.scaling = {"v": scale}
+            self.active_adapters = ["v"]
+            self.merged = False
+            self.disable_adapters = False
+
+        def get_delta_weight(self, a):
+            return (self.lora_B[a].weight @ self.lora_A[a].weight) * self.scaling[a]
+
+    class Attn(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.q_proj = LoraLinear(torch.nn.Linear(8, 8, bias=False))
+            self.q_norm = torch.nn.LayerNorm(8)
+
+    class Wrapped(torch.nn.Module):       # PeftModel naming: base_model.model.<decoder keys>
+        def __init__(self):
+            super().__init__()
+            self.base_model = torch.nn.Module()
+            self.base_model.model = torch.nn.Module()
+            self.base_model.model.layers = torch.nn.ModuleList([torch.nn.Module()])
+            self.base_model.model.layers[0].self_attn = Attn()
+
+    m = Wrapped()
+    sd = merged_decoder_state_dict(m)
+    q = m.base_model.model.layers[0].self_attn.q_proj
+    want = q.base_layer.weight + q.get_delta_weight("v")
+    assert torch.allclose(sd["layers.0.self_attn.q_proj.weight"], want)
+    assert "layers.0.self_attn.q_norm.weight" in sd
+    assert not any("lora" in k or "base_layer" in k for k in sd)
+    q.disable_adapters = True
+    assert torch.equal(merged_decoder_state_dict(m)["layers.0.self_attn.q_proj.weight"], q.base_layer.weight)

@@ -371,3 +371,28 @@ def test_uniform_null_rows_closed_form(gpu_device):
     torch.cuda.synchronize()
     assert torch.equal(again, full)
     rt.close()
+
+
+def test_weight_reload_matches_fresh_handle(gpu_device):
+    """LoRA re-pack hook (§8f row 3): re-loading changed weights into a live handle
+    (acehip.integration.refresh_decoder_weights) equals a handle built from them."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=2, window=8)
+    W1 = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=1, mode="parity").items()}
+    W2 = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=2, mode="parity").items()}
+    g = torch.Generator().manual_seed(9)
+    xt = torch.randn(1, 40, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(1, 40, 128, generator=g).bfloat16().to(gpu_device)
+    enc = torch.randn(1, 12, cfg.hidden_size, generator=g).bfloat16().to(gpu_device)
+    t = torch.tensor([0.5], dtype=torch.float32, device=gpu_device)
+    a = DiTRuntime(cfg, 0, max_S=32, max_Bc=1, max_Lenc=16)
+    a.load(W1)
+    a.load(W2)                       # the refresh path
+    a.set_condition(enc)
+    b = DiTRuntime(cfg, 0, max_S=32, max_Bc=1, max_Lenc=16)
+    b.load(W2)
+    b.set_condition(enc)
+    va, vb = a.forward(xt, ctx, t), b.forward(xt, ctx, t)
+    torch.cuda.synchronize()
+    assert torch.equal(va, vb)
+    a.close(); b.close()
