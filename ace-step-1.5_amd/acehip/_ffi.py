@@ -24,7 +24,7 @@ EXPORTS = [
     "acehip_dit_profile", "acehip_dit_profile_read", "acehip_dit_profile_kinds",
     "acehip_sampler_apg_euler", "acehip_sampler_adg_euler", "acehip_sampler_axpy",
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
-    "acehip_vae_encode", "acehip_vae_destroy",
+    "acehip_vae_encode", "acehip_vae_destroy", "acehip_wav_peak_normalize",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
     "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16", "acehip_attention_masked_bf16",
     "acehip_enc_create", "acehip_enc_set_weight", "acehip_enc_finalize", "acehip_enc_embed",
@@ -82,6 +82,7 @@ def _declare(lib):
         "acehip_vae_decode": (c_int, [P, P, c_int, c_int, P, P]),
         "acehip_vae_encode": (c_int, [P, P, c_int, c_int, P, P, P]),
         "acehip_vae_destroy": (c_int, [P]),
+        "acehip_wav_peak_normalize": (c_int, [P, c_int, c_int64, P, P]),
         "acehip_gemm_bf16": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
         "acehip_gemm_bf16_ex": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, c_int,
                                         c_int, P]),

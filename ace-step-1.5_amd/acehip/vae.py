@@ -66,6 +66,17 @@ class OobleckBackend:
         check(lib().acehip_vae_decode(self.h, ptr(z), B, T, ptr(out), stream_ptr()), "vae_decode")
         return out
 
+    def peak_normalize_(self, wav: torch.Tensor) -> torch.Tensor:
+        """In place: songs whose peak |x| exceeds 1 are divided by it — the decode
+        output guard of ``_decode_generate_music_pred_latents``
+        (generate_music_decode.py:190-192).  wav fp32 [B, C, N] on the device."""
+        assert wav.dtype == torch.float32 and wav.is_contiguous()
+        B = wav.shape[0]
+        peak = torch.empty(B, device=wav.device, dtype=torch.float32)
+        check(lib().acehip_wav_peak_normalize(ptr(wav), B, wav.numel() // B, ptr(peak), stream_ptr()),
+              "wav_peak_normalize")
+        return wav
+
     def decode(self, z: torch.Tensor):
         """diffusers-style: ``.decode(z).sample``."""
         return SimpleNamespace(sample=self.decode_tensor(z))

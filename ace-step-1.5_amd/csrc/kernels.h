@@ -92,6 +92,8 @@ int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance,
               float dt, int out_mode, hipStream_t s);
 
 // ----------------------------------------------------------------- misc ----
+// per song b: peak = max |wav[b]|; if peak > 1, wav[b] /= peak (n samples per song, n % 4 == 0)
+int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s);
 int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s);
 
 }  // namespace acehip

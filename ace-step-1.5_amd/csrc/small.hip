@@ -131,7 +131,49 @@ __global__ void add_row_bcast_kernel(bf16_t *X, const bf16_t *c, int64_t n8, int
     ((uint4 *)X)[i] = pack8(x);
 }
 
+__global__ __launch_bounds__(256) void wav_peak_kernel(const float4 *w, int64_t n4, unsigned *peak) {
+    const int b = blockIdx.y;
+    const float4 *p = w + (int64_t)b * n4;
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 v = p[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        atomicMax(peak + b, __float_as_uint(m));   // non-negative floats order as their bits
+    }
+}
+
+__global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, const float *peak) {
+    const int b = blockIdx.y;
+    const float pk = peak[b];
+    if (!(pk > 1.0f)) return;
+    float4 *p = w + (int64_t)b * n4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        float4 v = p[i];
+        v.x /= pk; v.y /= pk; v.z /= pk; v.w /= pk;
+        p[i] = v;
+    }
+}
+
 }  // namespace
+
+int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s) {
+    HIP_TRY(hipMemsetAsync(peak, 0, (size_t)B * sizeof(float), s));
+    const int64_t n4 = n / 4;
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, (n4 + 255) / 256);
+    wav_peak_kernel<<<dim3(gx, B), 256, 0, s>>>((const float4 *)wav, n4, (unsigned *)peak);
+    HIP_TRY(hipGetLastError());
+    wav_scale_kernel<<<dim3(gx, B), 256, 0, s>>>((float4 *)wav, n4, peak);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int gather_head_row(const bf16_t *V, int KV, int Le, int H, bf16_t *out, hipStream_t s) {
     if (KV <= 0 || H % KV) return fail(-1, "gather_head_row: heads");

@@ -423,4 +423,14 @@ int acehip_vae_destroy(acehip_vae *h) {
     return 0;
 }
 
+// _decode_generate_music_pred_latents' output guard (generate_music_decode.py:190-192):
+// peak = |wav|.amax over (channels, samples) per song; if any peak > 1 every song
+// is divided by max(peak, 1) — per song that is "divide by peak when peak > 1",
+// IEEE division as torch does it.  wav fp32 [B][n] in place; peak: [B] scratch.
+int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *stream) {
+    if (!wav || !peak || B <= 0 || n <= 0) return fail(ACEHIP_E_ARG, "wav_peak_normalize: argument");
+    if (n % 4) return fail(ACEHIP_E_ARG, "wav_peak_normalize: samples per song must be a multiple of 4");
+    return wav_peak_normalize(wav, B, n, peak, (hipStream_t)stream);
+}
+
 }  // extern "C"

@@ -197,6 +197,7 @@ def main():
         e1.record()
         if vae is not None:
             wav = vae.decode_tensor(res["target_latents"].transpose(1, 2))
+            vae.peak_normalize_(wav)          # decode output guard (generate_music_decode.py:190-192)
         e2.record()
         return e0, e1, e2
 

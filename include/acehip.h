@@ -240,6 +240,13 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
 
 int acehip_vae_destroy(acehip_vae *h);
 
+/* The decode output guard of _decode_generate_music_pred_latents
+ * (acestep/core/generation/handler/generate_music_decode.py:190-192):
+ * per song, peak = max |wav|; if peak > 1 the song is divided by its peak.
+ * wav fp32 [B, n] in place (n = channels·samples, n % 4 == 0); peak: device
+ * scratch of B floats (receives the peaks). */
+int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *stream);
+
 /* ------------------------------------------------------------ kernels ---- */
 /* Single-kernel entry points used by the parity tests and the profiler
  * (same code the runtimes above launch). */

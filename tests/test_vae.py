@@ -89,3 +89,24 @@ def test_vae_encode_parity(gpu_device, cfg_name):
     assert rel_l2(mean, ref_mean) < 0.03, rel_l2(mean, ref_mean)
     assert rel_l2(smp, ref_s) < 0.03
     be.close()
+
+
+@pytest.mark.gpu
+def test_wav_peak_normalize(gpu_device):
+    """generate_music_decode.py:190-192 output guard, bit-exact vs the torch formula."""
+    from acehip.vae import OobleckBackend
+    from acehip.config import VAEConfig
+    be = OobleckBackend(VAEConfig.tiny(), 0, max_T=8, with_encoder=False)
+    g = torch.Generator().manual_seed(4)
+    wav = torch.randn(3, 2, 3840 * 5, generator=g)
+    wav[0] *= 0.2            # peak < 1: untouched
+    wav[1] *= 2.5            # peak > 1: divided
+    wav[2, 1, 77] = -7.0     # negative extreme sets the peak
+    ref = wav.clone()
+    peak = ref.abs().amax(dim=[1, 2], keepdim=True)
+    if torch.any(peak > 1.0):
+        ref = ref / peak.clamp(min=1.0)
+    out = be.peak_normalize_(wav.to(gpu_device).contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
+    be.close()
