@@ -28,7 +28,7 @@ EXPORTS = [
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
     "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16", "acehip_attention_masked_bf16",
     "acehip_enc_create", "acehip_enc_set_weight", "acehip_enc_finalize", "acehip_enc_embed",
-    "acehip_enc_forward", "acehip_enc_destroy",
+    "acehip_enc_forward", "acehip_enc_destroy", "acehip_fsq_quantize", "acehip_fsq_codes_from_indices",
 ]
 
 
@@ -96,6 +96,8 @@ def _declare(lib):
         "acehip_enc_embed": (c_int, [P, P, c_int, P, P]),
         "acehip_enc_forward": (c_int, [P, P, P, c_int, c_int, P, P]),
         "acehip_enc_destroy": (c_int, [P]),
+        "acehip_fsq_quantize": (c_int, [P, c_int, c_int, POINTER(c_int), c_int, P, c_int, P, P]),
+        "acehip_fsq_codes_from_indices": (c_int, [P, c_int, POINTER(c_int), c_int, P, c_int, P]),
         "acehip_rmsnorm_bf16": (c_int, [P, P, P, P, c_int64, c_int, P, c_int, c_int, c_float, c_int, P]),
         "acehip_gemm_headpost_bf16": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                               P, P, P, P, c_float, P, P, P, P]),

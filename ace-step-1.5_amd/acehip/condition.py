@@ -11,12 +11,15 @@ Every Linear / encoder layer / norm runs in libacehip (``acehip_enc_*``,
 plumbing (stable argsort + gather) done with torch ops on the device, exactly
 as the reference does them.  There is no CPU or eager fallback.
 
-``HipPrepareCondition`` mirrors ``prepare_condition`` (base:1607-1652) for
-the text2music / repaint cases (no audio-code hints needed, or precomputed
-hints given).  Cover songs that need the FSQ audio tokenizer
-(``vector_quantize_pytorch.ResidualFSQ``, not built here — SURVEY §8f row 2)
-are routed to the reference's own ``prepare_condition`` when one is given,
-otherwise they raise.
+``AudioTokenizer`` / ``AudioDetokenizer`` are the cover
+path's AceStepAudioTokenizer (attention pooler + FSQ) and AudioTokenDetokenizer
+on the same encoder-stack runtime; the FSQ is a restatement of
+``vector_quantize_pytorch`` (absent here: parity unpinned).
+
+``HipPrepareCondition`` mirrors ``prepare_condition`` (base:1607-1652): the
+encoders always, the tokenizer → detokenizer LM hints when a song is a cover
+(with the tokenizer handles given; otherwise such songs go to the reference's
+own ``prepare_condition`` when one is given, or raise).
 """
 from __future__ import annotations
 
@@ -168,6 +171,8 @@ class ConditionEncoder:
                         rope_theta=float(getattr(c, "rope_theta", 1e6)), layer_types=list(c.layer_types),
                         num_lyric_encoder_hidden_layers=c.num_lyric_encoder_hidden_layers,
                         num_timbre_encoder_hidden_layers=c.num_timbre_encoder_hidden_layers,
+                        num_attention_pooler_hidden_layers=c.num_attention_pooler_hidden_layers,
+                        pool_window_size=c.pool_window_size, audio_acoustic_hidden_dim=c.audio_acoustic_hidden_dim,
                         text_hidden_dim=c.text_hidden_dim, timbre_hidden_dim=c.timbre_hidden_dim)
         dev = next(model.parameters()).device
         ce = cls(cfg, dev.index or 0, **kw)
@@ -215,6 +220,119 @@ class ConditionEncoder:
         self.timbre.close()
 
 
+FSQ_LEVELS = (8, 8, 8, 5, 5, 5)      # configuration_acestep_v15.py:152
+
+
+def _gemm(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """bf16 x [.., K] · Wᵀ (+ b) on libacehip (N % 128, K % 64)."""
+    x = x.contiguous()
+    M, K = x.numel() // x.shape[-1], x.shape[-1]
+    N = W.shape[0]
+    out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.bfloat16)
+    check(lib().acehip_gemm_bf16(ptr(x), K, ptr(W), K, ptr(out), N, M, N, K, ptr(b), stream_ptr()), "gemm")
+    return out
+
+
+def _pad_rows(w: torch.Tensor, rows: int, dev) -> torch.Tensor:
+    out = torch.zeros(rows, *w.shape[1:], device=dev, dtype=torch.bfloat16)
+    out[: w.shape[0]] = w.detach().to(dev, torch.bfloat16)
+    return out.contiguous()
+
+
+class AudioTokenizer:
+    """AceStepAudioTokenizer (base:1181-1223) on libacehip: audio_acoustic_proj →
+    AttentionPooler (base:734-859: embed, special token first, encoder layers on
+    (P+1)-token sequences, norm, CLS) → ResidualFSQ (project_in → FSQ → project_out;
+    the FSQ restated from vector_quantize_pytorch's published algorithm — the
+    library is not in this image, so its parity is unpinned)."""
+
+    def __init__(self, cfg: DiTConfig, device: int = 0, max_patches: int = 3000):
+        self.cfg, self.P = cfg, cfg.pool_window_size
+        self.device = torch.device("cuda", device)
+        self.pooler = EncoderStack(cfg, cfg.num_attention_pooler_hidden_layers, cfg.hidden_size, True,
+                                   device=device, max_tokens=max_patches * (self.P + 1), max_S=self.P + 1)
+        self._levels = (_ffi.c_int * len(FSQ_LEVELS))(*FSQ_LEVELS)
+
+    def load(self, weights: Dict[str, torch.Tensor], prefix: str = "tokenizer."):
+        w = {k[len(prefix):]: v for k, v in weights.items() if k.startswith(prefix)}
+        dev = self.device
+        self.w_proj = w["audio_acoustic_proj.weight"].detach().to(dev, torch.bfloat16).contiguous()
+        self.b_proj = w["audio_acoustic_proj.bias"].detach().to(dev, torch.bfloat16).contiguous()
+        self.pooler.load(w, "attention_pooler.")
+        nl = len(FSQ_LEVELS)
+        # project_in [6, D] rows padded to 128; project_out [D, 6] columns padded to 64 (K)
+        self.w_in = _pad_rows(w["quantizer.project_in.weight"], 128, dev)
+        self.b_in = _pad_rows(w["quantizer.project_in.bias"], 128, dev)
+        wo = torch.zeros(w["quantizer.project_out.weight"].shape[0], 64, device=dev, dtype=torch.bfloat16)
+        wo[:, :nl] = w["quantizer.project_out.weight"].detach().to(dev, torch.bfloat16)
+        self.w_out = wo.contiguous()
+        self.b_out = w["quantizer.project_out.bias"].detach().to(dev, torch.bfloat16).contiguous()
+
+    def project_out(self, codes64: torch.Tensor) -> torch.Tensor:
+        return _gemm(codes64, self.w_out, self.b_out)
+
+    def quantize(self, h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """ResidualFSQ.forward (1 quantizer): h [.., D] → (quantized [.., D], indices [.., 1] int32)."""
+        z = _gemm(h, self.w_in, self.b_in)                        # [.., 128], first 6 columns real
+        M = z.numel() // 128
+        codes = torch.empty(M, 64, device=self.device, dtype=torch.bfloat16)
+        idx = torch.empty(M, device=self.device, dtype=torch.int32)
+        check(lib().acehip_fsq_quantize(ptr(z), 128, M, self._levels, len(FSQ_LEVELS), ptr(codes), 64, ptr(idx),
+                                        stream_ptr()), "fsq_quantize")
+        q = self.project_out(codes).view(*h.shape[:-1], -1)
+        return q, idx.view(*h.shape[:-1], 1)
+
+    def get_output_from_indices(self, indices: torch.Tensor) -> torch.Tensor:
+        """ResidualFSQ.get_output_from_indices (used by audio_codes.py:62): [.., 1] → [.., D]."""
+        idx = indices.to(self.device, torch.int32).contiguous()
+        M = idx.numel()
+        codes = torch.empty(M, 64, device=self.device, dtype=torch.bfloat16)
+        check(lib().acehip_fsq_codes_from_indices(ptr(idx), M, self._levels, len(FSQ_LEVELS), ptr(codes), 64,
+                                                  stream_ptr()), "fsq_codes")
+        return self.project_out(codes).view(*indices.shape[:-1], -1)
+
+    def attention_pooler(self, x: torch.Tensor) -> torch.Tensor:
+        """x [N, T, P, D] (embedded by audio_acoustic_proj) → CLS [N, T, D]."""
+        N, T, P, D = x.shape
+        h = self.pooler.embed(x)
+        sp = self.pooler.extra["special_token"].expand(N, T, 1, D)
+        h = torch.cat([sp, h], dim=2).reshape(N * T, P + 1, D)
+        return self.pooler.forward(h, None)[:, 0, :].reshape(N, T, D)
+
+    def __call__(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """AceStepAudioTokenizer.forward: x [N, T/P, P, 64] → (quantized, indices)."""
+        h = _gemm(x.to(self.device, torch.bfloat16), self.w_proj, self.b_proj)
+        return self.quantize(self.attention_pooler(h))
+
+    def close(self):
+        self.pooler.close()
+
+
+class AudioDetokenizer:
+    """AudioTokenDetokenizer (base:862-994) on libacehip: embed, repeat each token
+    P times + the learned special tokens (a bf16 add, as the reference), encoder
+    layers on P-token sequences, norm, proj_out → 25 Hz latents."""
+
+    def __init__(self, cfg: DiTConfig, device: int = 0, max_patches: int = 3000):
+        self.cfg, self.P = cfg, cfg.pool_window_size
+        self.stack = EncoderStack(cfg, cfg.num_attention_pooler_hidden_layers, cfg.hidden_size, True,
+                                  out_dim=cfg.audio_acoustic_hidden_dim, device=device,
+                                  max_tokens=max_patches * self.P, max_S=self.P)
+
+    def load(self, weights: Dict[str, torch.Tensor], prefix: str = "detokenizer."):
+        self.stack.load(weights, prefix)
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        N, T, D = x.shape
+        h = self.stack.embed(x)
+        h = h.unsqueeze(2).repeat(1, 1, self.P, 1) + self.stack.extra["special_tokens"].expand(N, T, -1, -1)
+        out = self.stack.forward(h.reshape(N * T, self.P, D), None)
+        return out.reshape(N, T * self.P, -1)
+
+    def close(self):
+        self.stack.close()
+
+
 class HipPrepareCondition:
     """Drop-in for ``AceStepConditionGenerationModel.prepare_condition``
     (base:1607-1652) with the encoders on libacehip.
@@ -225,9 +343,20 @@ class HipPrepareCondition:
     Covers that need the tokenizer go to ``fallback`` (the reference's own
     ``prepare_condition``) or raise."""
 
-    def __init__(self, encoder: ConditionEncoder, fallback: Optional[Callable] = None):
+    def __init__(self, encoder: ConditionEncoder, fallback: Optional[Callable] = None,
+                 tokenizer: Optional[AudioTokenizer] = None, detokenizer: Optional[AudioDetokenizer] = None):
         self.encoder = encoder
         self.fallback = fallback
+        self.tokenizer, self.detokenizer = tokenizer, detokenizer
+
+    def tokenize(self, x, silence_latent):
+        """AceStepConditionGenerationModel.tokenize (base:1580-1591): pad T to a
+        multiple of P with the silence latent, group P frames, tokenize."""
+        P = self.tokenizer.P
+        if x.shape[1] % P:
+            pad = P - x.shape[1] % P
+            x = torch.cat([x, silence_latent[:1, :pad].to(x.dtype).repeat(x.shape[0], 1, 1)], dim=1)
+        return self.tokenizer(x.reshape(x.shape[0], -1, P, x.shape[-1]))
 
     def __call__(self, text_hidden_states, text_attention_mask, lyric_hidden_states, lyric_attention_mask,
                  refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask, hidden_states,
@@ -235,6 +364,14 @@ class HipPrepareCondition:
                  precomputed_lm_hints_25Hz=None, audio_codes=None):
         need_tokenizer = precomputed_lm_hints_25Hz is None and (
             audio_codes is not None or bool((is_covers > 0).any()))
+        if need_tokenizer and self.tokenizer is not None and self.detokenizer is not None:
+            # base:1641-1649: LM hints from the source latents (or from audio codes)
+            if audio_codes is not None:
+                q = self.tokenizer.get_output_from_indices(audio_codes)
+            else:
+                q, _ = self.tokenize(hidden_states.to(torch.bfloat16), silence_latent)
+            precomputed_lm_hints_25Hz = self.detokenizer(q).to(hidden_states.dtype)
+            need_tokenizer = False
         if need_tokenizer:
             if self.fallback is None:
                 raise NotImplementedError("acehip: cover conditioning needs the FSQ audio tokenizer "

@@ -16,8 +16,8 @@ Seams:
   * cond   — ``prepare_condition`` (``base:1607-1652``, called from
              ``generate_audio`` ``base:1820``): replaced by
              :class:`~acehip.condition.HipPrepareCondition` (text projector, lyric
-             and timbre encoders on libacehip); cover conditioning that needs the
-             FSQ audio tokenizer goes to the reference's own ``prepare_condition``.
+             and timbre encoders, and for covers the audio tokenizer (pooler + FSQ)
+             and detokenizer, all on libacehip).
   * LoRA   — ``add_lora`` / ``remove_lora`` / ``unload_lora`` / ``set_lora_scale`` /
              ``set_use_lora`` / ``set_active_lora_adapter`` (``handler/lora/lifecycle.py:164-420``,
              ``lora/controls.py:12-157``) change the decoder's effective weights;
@@ -37,7 +37,7 @@ from typing import Optional
 
 import torch
 
-from .condition import ConditionEncoder, HipPrepareCondition
+from .condition import AudioDetokenizer, AudioTokenizer, ConditionEncoder, HipPrepareCondition
 from .config import VAEConfig
 from .dit import AceStepDiTBackend
 from .vae import OobleckBackend
@@ -115,7 +115,17 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
                                                  max_batch=max_batch)
     if condition:
         ce = ConditionEncoder.from_reference_model(handler.model, max_batch=max_batch)
-        dit.prepare_condition = HipPrepareCondition(ce, fallback=handler.model.prepare_condition)
+        tok = det = None
+        m = handler.model
+        if getattr(m, "tokenizer", None) is not None and getattr(m, "detokenizer", None) is not None:
+            dev = ce.device.index or 0
+            patches = int(max_seconds * 25) // ce.cfg.pool_window_size + 1
+            tok = AudioTokenizer(ce.cfg, dev, max_patches=max_batch * patches)
+            tok.load({"tokenizer." + k: v for k, v in m.tokenizer.state_dict().items()})
+            det = AudioDetokenizer(ce.cfg, dev, max_patches=max_batch * patches)
+            det.load({"detokenizer." + k: v for k, v in m.detokenizer.state_dict().items()})
+        dit.prepare_condition = HipPrepareCondition(ce, fallback=m.prepare_condition, tokenizer=tok,
+                                                    detokenizer=det)
     orig_generate = handler.model.generate_audio
 
     def generate_audio(**kw):

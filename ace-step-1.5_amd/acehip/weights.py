@@ -106,6 +106,29 @@ def condenc_weight_shapes(cfg: DiTConfig) -> Dict[str, Shape]:
     return s
 
 
+def tokenizer_weight_shapes(cfg: DiTConfig) -> Dict[str, Shape]:
+    """AceStepAudioTokenizer (base:1189-1203) under ``tokenizer.`` and
+    AudioTokenDetokenizer (base:870-886) under ``detokenizer.``; the quantizer is
+    ResidualFSQ(dim=fsq_dim, levels [8,8,8,5,5,5]) → project_in / project_out."""
+    D, nl = cfg.hidden_size, 6
+    s: Dict[str, Shape] = {"tokenizer.audio_acoustic_proj.weight": (D, cfg.audio_acoustic_hidden_dim),
+                           "tokenizer.audio_acoustic_proj.bias": (D,)}
+    s.update(encoder_stack_shapes(cfg, "tokenizer.attention_pooler", cfg.num_attention_pooler_hidden_layers, D, True))
+    s["tokenizer.attention_pooler.special_token"] = (1, 1, D)
+    s["tokenizer.quantizer.project_in.weight"] = (nl, D)
+    s["tokenizer.quantizer.project_in.bias"] = (nl,)
+    s["tokenizer.quantizer.project_out.weight"] = (D, nl)
+    s["tokenizer.quantizer.project_out.bias"] = (D,)
+    s.update(encoder_stack_shapes(cfg, "detokenizer", cfg.num_attention_pooler_hidden_layers, D, True,
+                                  out_dim=cfg.audio_acoustic_hidden_dim))
+    s["detokenizer.special_tokens"] = (1, cfg.pool_window_size, D)
+    return s
+
+
+def synth_tokenizer_weights(cfg: DiTConfig, seed: int = 0, mode: str = "bench", **kw):
+    return synth_weights(tokenizer_weight_shapes(cfg), seed, mode, **kw)
+
+
 def synth_condenc_weights(cfg: DiTConfig, seed: int = 0, mode: str = "bench", **kw):
     return synth_weights(condenc_weight_shapes(cfg), seed, mode, **kw)
 

@@ -299,4 +299,21 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
     return 0;
 }
 
+int acehip_fsq_quantize(const void *z, int ldz, int M, const int *levels, int n_levels, void *codes, int ldc,
+                        int32_t *indices, void *stream) {
+    if (!z || !codes || !levels || n_levels <= 0 || n_levels > 8 || ldz < n_levels)
+        return fail(ACEHIP_E_ARG, "fsq_quantize: argument");
+    FsqLevels lv{n_levels, {}};
+    for (int i = 0; i < n_levels; ++i) lv.L[i] = levels[i];
+    return fsq_quantize((const bf16_t *)z, ldz, M, lv, (bf16_t *)codes, ldc, indices, (hipStream_t)stream);
+}
+
+int acehip_fsq_codes_from_indices(const int32_t *indices, int M, const int *levels, int n_levels, void *codes,
+                                  int ldc, void *stream) {
+    if (!indices || !codes || !levels || n_levels <= 0 || n_levels > 8) return fail(ACEHIP_E_ARG, "fsq_codes: argument");
+    FsqLevels lv{n_levels, {}};
+    for (int i = 0; i < n_levels; ++i) lv.L[i] = levels[i];
+    return fsq_codes_from_indices(indices, M, lv, (bf16_t *)codes, ldc, (hipStream_t)stream);
+}
+
 }  // extern "C"

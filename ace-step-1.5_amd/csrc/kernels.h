@@ -91,6 +91,13 @@ int axpy_bf16(const bf16_t *vt, bf16_t *xt, int64_t n, float sc, hipStream_t s);
 int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance, float sigma,
               float dt, int out_mode, hipStream_t s);
 
+// ------------------------------------------------------------------ FSQ ----
+struct FsqLevels { int n; int L[8]; };
+// z [M][ldz] bf16 (first n columns) → codes [M][ldc ≥ 64] bf16 (columns ≥ n zeroed), idx [M] (or null)
+int fsq_quantize(const bf16_t *z, int64_t ldz, int M, const FsqLevels &lv, bf16_t *codes, int64_t ldc, int *idx,
+                 hipStream_t s);
+int fsq_codes_from_indices(const int *idx, int M, const FsqLevels &lv, bf16_t *codes, int64_t ldc, hipStream_t s);
+
 // ----------------------------------------------------------------- misc ----
 // per song b: peak = max |wav[b]|; if peak > 1, wav[b] /= peak (n samples per song, n % 4 == 0)
 int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s);

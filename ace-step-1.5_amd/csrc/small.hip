@@ -162,7 +162,60 @@ __global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, c
     }
 }
 
+// FSQ (vector_quantize_pytorch FSQ.bound / codes_to_indices, restated; see
+// oracle/condenc_oracle.py): fp32 math as the library forces (force_quantization_f32)
+__global__ void fsq_quantize_kernel(const bf16_t *z, int64_t ldz, int M, FsqLevels lv, bf16_t *codes, int64_t ldc,
+                                    int *idx) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= M) return;
+    float index = 0.f, basis = 1.f;
+    for (int i = 0; i < lv.n; ++i) {
+        const int L = lv.L[i];
+        const float half_l = ((float)(L - 1) * 1.001f) / 2.0f;
+        const float offset = (L % 2 == 0) ? 0.5f : 0.0f;
+        const float shift = atanhf(offset / half_l);
+        const float bounded = tanhf(bf2f(z[(int64_t)row * ldz + i]) + shift) * half_l - offset;
+        const float hw = (float)(L / 2);
+        const float code = rintf(bounded) / hw;                 // torch.round: half to even
+        codes[(int64_t)row * ldc + i] = f2bf(code);
+        index += (code * hw + hw) * basis;
+        basis *= (float)L;
+    }
+    for (int i = lv.n; i < 64; ++i) codes[(int64_t)row * ldc + i] = 0;   // K padding of project_out
+    if (idx) idx[row] = (int)rintf(index);
+}
+
+__global__ void fsq_codes_kernel(const int *idx, int M, FsqLevels lv, bf16_t *codes, int64_t ldc) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= M) return;
+    int basis = 1;
+    for (int i = 0; i < lv.n; ++i) {
+        const int L = lv.L[i], hw = L / 2;
+        const int level = (idx[row] / basis) % L;
+        codes[(int64_t)row * ldc + i] = f2bf((float)(level - hw) / (float)hw);
+        basis *= L;
+    }
+    for (int i = lv.n; i < 64; ++i) codes[(int64_t)row * ldc + i] = 0;
+}
+
 }  // namespace
+
+int fsq_quantize(const bf16_t *z, int64_t ldz, int M, const FsqLevels &lv, bf16_t *codes, int64_t ldc, int *idx,
+                 hipStream_t s) {
+    if (M <= 0) return 0;
+    if (lv.n <= 0 || lv.n > 8 || ldc < 64) return fail(-1, "fsq_quantize: 1..8 levels, ldc >= 64");
+    fsq_quantize_kernel<<<(M + 255) / 256, 256, 0, s>>>(z, ldz, M, lv, codes, ldc, idx);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int fsq_codes_from_indices(const int *idx, int M, const FsqLevels &lv, bf16_t *codes, int64_t ldc, hipStream_t s) {
+    if (M <= 0) return 0;
+    if (lv.n <= 0 || lv.n > 8 || ldc < 64) return fail(-1, "fsq_codes: 1..8 levels, ldc >= 64");
+    fsq_codes_kernel<<<(M + 255) / 256, 256, 0, s>>>(idx, M, lv, codes, ldc);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s) {
     HIP_TRY(hipMemsetAsync(peak, 0, (size_t)B * sizeof(float), s));

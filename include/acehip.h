@@ -172,6 +172,18 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
                        void *stream);
 int acehip_enc_destroy(acehip_enc *h);
 
+/* FSQ quantizer of the audio tokenizer (ResidualFSQ, 1 quantizer, levels
+ * {8,8,8,5,5,5}: base:1196-1200; vector_quantize_pytorch FSQ restated, see
+ * oracle/condenc_oracle.py): z bf16 [M, ldz] (the project_in output, first
+ * n_levels columns) → codes bf16 [M, ldc >= 64] (columns >= n_levels zeroed, so
+ * the padded project_out GEMM can consume them) and int32 indices [M] (or NULL). */
+int acehip_fsq_quantize(const void *z, int ldz, int M, const int *levels, int n_levels, void *codes, int ldc,
+                        int32_t *indices, void *stream);
+/* FSQ.indices_to_codes (quantizer.get_output_from_indices before project_out,
+ * acestep/core/generation/handler/audio_codes.py:62). */
+int acehip_fsq_codes_from_indices(const int32_t *indices, int M, const int *levels, int n_levels, void *codes,
+                                  int ldc, void *stream);
+
 /* ------------------------------------------------------------ sampler ---- */
 
 /* One base/sft CFG step: cond/uncond split + APG (momentum -0.75, norm clip

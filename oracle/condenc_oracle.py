@@ -156,3 +156,57 @@ def detokenizer(W, cfg, x: Tensor, p: str = "detokenizer") -> Tensor:
     h = encoder_body(W, p, cfg, cfg.num_attention_pooler_hidden_layers, h, None)
     h = F.linear(h, W[f"{p}.proj_out.weight"], W[f"{p}.proj_out.bias"])
     return h.reshape(B, T * P, -1)
+
+
+# ---------------------------------------------------------------------------
+# FSQ — vector_quantize_pytorch (>= 1.27.15, reference requirements.txt:34) is NOT
+# in this container, so this is a restatement of its published algorithm
+# (ResidualFSQ with num_quantizers = 1 over FSQ(levels)), PARITY UNPINNED:
+#   ResidualFSQ.forward: z = project_in(x) (Linear dim→len(levels), bias);
+#     quantized = FSQ(z / scale_0) · scale_0 with scale_0 = (levels−1)^0 = 1;
+#     out = project_out(quantized) (Linear len(levels)→dim, bias)
+#   FSQ.forward (force_quantization_f32): z.float();
+#     half_l = (L−1)(1+1e-3)/2; offset = 0.5 if L even else 0; shift = atanh(offset/half_l)
+#     bounded = tanh(z + shift)·half_l − offset; codes = round(bounded) / (L // 2)
+#     indices = Σ_i (codes_i·(L_i//2) + L_i//2) · basis_i, basis = cumprod([1] + L[:-1])
+#   codes cast back to the input dtype before project_out.
+FSQ_LEVELS = [8, 8, 8, 5, 5, 5]     # configuration_acestep_v15.py:152
+
+
+def fsq_quantize(z: Tensor, levels=FSQ_LEVELS) -> Tuple[Tensor, Tensor]:
+    """z [..., len(levels)] (model dtype) → (codes in z's dtype, int32 indices [...])."""
+    dt = z.dtype
+    L = torch.tensor(levels, dtype=torch.int32)
+    zf = z.float()
+    half_l = (L - 1) * (1 + 1e-3) / 2
+    offset = torch.where(L % 2 == 0, 0.5, 0.0)
+    shift = (offset / half_l).atanh()
+    bounded = (zf + shift).tanh() * half_l - offset
+    hw = L // 2
+    codes = bounded.round() / hw
+    basis = torch.cumprod(torch.tensor([1] + levels[:-1]), dim=0, dtype=torch.int32)
+    idx = ((codes * hw + hw) * basis).sum(dim=-1).round().to(torch.int32)
+    return codes.to(dt), idx
+
+
+def fsq_codes_from_indices(idx: Tensor, dtype, levels=FSQ_LEVELS) -> Tensor:
+    """FSQ.indices_to_codes: level_i = (idx // basis_i) % L_i, code = (level − L//2)/(L//2)."""
+    L = torch.tensor(levels, dtype=torch.int64)
+    basis = torch.cumprod(torch.tensor([1] + levels[:-1]), dim=0)
+    lv = (idx.long().unsqueeze(-1) // basis) % L
+    hw = L // 2
+    return ((lv - hw).float() / hw).to(dtype)
+
+
+def residual_fsq(W, x: Tensor, p: str = "tokenizer.quantizer") -> Tuple[Tensor, Tensor]:
+    z = F.linear(x, W[f"{p}.project_in.weight"], W[f"{p}.project_in.bias"])
+    codes, idx = fsq_quantize(z)
+    return F.linear(codes, W[f"{p}.project_out.weight"], W[f"{p}.project_out.bias"]), idx
+
+
+def audio_tokenizer(W, cfg, x: Tensor) -> Tuple[Tensor, Tensor]:
+    """AceStepAudioTokenizer.forward (base:1206-1218): x [N, T/P, P, 64] →
+    (quantized [N, T/P, D], indices [N, T/P])."""
+    h = F.linear(x, W["tokenizer.audio_acoustic_proj.weight"], W["tokenizer.audio_acoustic_proj.bias"])
+    h = attention_pooler(W, cfg, h)
+    return residual_fsq(W, h)

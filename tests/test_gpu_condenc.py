@@ -103,3 +103,71 @@ def test_prepare_condition_dropin(gpu_device):
            hidden_states=src, attention_mask=None, silence_latent=None, src_latents=src, chunk_masks=cm,
            is_covers=torch.ones(2, dtype=torch.long, device=d))
     ce.close()
+
+
+@pytest.mark.parametrize("name", ["tiny_bfloat16", "tiny_float32"])
+def test_tokenizer_detokenizer_vs_reference(gpu_device, name):
+    """AttentionPooler / tokenizer (+ restated FSQ) / detokenizer on libacehip vs the
+    reference fixtures (tools/make_golden.py gen_tokenizer); codes may flip at a rounding
+    boundary in bf16, so indices are compared by agreement rate."""
+    from acehip.condition import AudioDetokenizer, AudioTokenizer
+    from acehip.weights import synth_tokenizer_weights
+    meta = golden_manifest()["tokenizer"][name]
+    cfg = DiTConfig(**meta["cfg"])
+    g = load_golden("tokenizer_" + name)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_tokenizer_weights(cfg, seed=meta["seed"],
+                                                                               mode="parity").items()}
+    tok = AudioTokenizer(cfg, 0, max_patches=64)
+    tok.load(W)
+    det = AudioDetokenizer(cfg, 0, max_patches=64)
+    det.load(W)
+    d = gpu_device
+    pooled = tok.attention_pooler(g["pooled_in"].to(d, torch.bfloat16))
+    x = g["x"].to(d, torch.bfloat16)
+    quant, idx = tok(x.reshape(x.shape[0], -1, cfg.pool_window_size, x.shape[-1]))
+    det_out = det(g["det_in"].to(d, torch.bfloat16))
+    hints = det(g["quantized"].to(d, torch.bfloat16))
+    torch.cuda.synchronize()
+    for out, ref in ((pooled, g["pooled"]), (det_out, g["det_out"]), (hints, g["hints"])):
+        assert out.shape == ref.shape
+        assert rel_l2(out.float().cpu(), ref.float()) < TOL_REL
+        assert cosine(out.float().cpu(), ref.float()) > TOL_COS
+    agree = (idx.cpu() == g["indices"]).float().mean()
+    assert agree > 0.9, float(agree)
+    # codes -> indices -> output round trip (quantizer.get_output_from_indices, audio_codes.py:62)
+    again = tok.get_output_from_indices(idx)
+    torch.cuda.synchronize()
+    assert torch.equal(again, quant)
+    tok.close(); det.close()
+
+
+def test_prepare_condition_cover(gpu_device):
+    """prepare_condition (base:1635-1651) with a cover song: LM hints = detokenize(tokenize(src
+    padded to a multiple of 5 with the silence latent))[:, :T] replace src where is_covers."""
+    from acehip.condition import AudioDetokenizer, AudioTokenizer, HipPrepareCondition
+    from acehip.weights import synth_tokenizer_weights
+    cfg, g, ce = _setup("tiny_bfloat16", gpu_device)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_tokenizer_weights(cfg, seed=5, mode="parity").items()}
+    tok, det = AudioTokenizer(cfg, 0, max_patches=32), AudioDetokenizer(cfg, 0, max_patches=32)
+    tok.load(W)
+    det.load(W)
+    d = gpu_device
+    T = 23                                      # not a multiple of the pool window: silence padding
+    src = torch.randn(2, T, 64, device=d).bfloat16()
+    sil = torch.randn(1, 40, 64, device=d).bfloat16()
+    cm = torch.ones(2, T, 64, device=d).bfloat16()
+    pc = HipPrepareCondition(ce, tokenizer=tok, detokenizer=det)
+    enc, mask, ctx = pc(text_hidden_states=g["text"].to(d), text_attention_mask=g["text_mask"].to(d),
+                        lyric_hidden_states=g["lyric"].to(d), lyric_attention_mask=g["lyric_mask"].to(d),
+                        refer_audio_acoustic_hidden_states_packed=g["refer"].to(d),
+                        refer_audio_order_mask=g["order"].to(d), hidden_states=src, attention_mask=None,
+                        silence_latent=sil, src_latents=src, chunk_masks=cm,
+                        is_covers=torch.tensor([1, 0], device=d))
+    xp = torch.cat([src, sil[:1, :2].repeat(2, 1, 1)], dim=1)
+    q, _ = tok(xp.reshape(2, -1, 5, 64))
+    hints = det(q)[:, :T]
+    torch.cuda.synchronize()
+    assert torch.equal(ctx[0, :, :64], hints[0])
+    assert torch.equal(ctx[1, :, :64], src[1])
+    assert torch.equal(ctx[:, :, 64:], cm)
+    ce.close(); tok.close(); det.close()

@@ -32,7 +32,7 @@ import torch
 from safetensors.torch import save_file
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(REPO, "ace-step-1.5_amd"))
+sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
 OUT = os.path.join(REPO, "tests", "golden")
 
 from acehip.config import DiTConfig  # noqa: E402
@@ -254,6 +254,59 @@ def gen_condenc(name, width, dtype, seed):
             "weights_checksum": checksum(W)}
 
 
+class _FsqRestated(torch.nn.Module):
+    """Stand-in for vector_quantize_pytorch.ResidualFSQ (absent here): the oracle's
+    restatement of its published algorithm, so the tokenizer fixture pins the
+    reference's projection + attention pooler around it (the FSQ part itself is
+    parity-unpinned)."""
+
+    def __init__(self, dim, levels, num_quantizers, **kw):
+        super().__init__()
+        self.project_in = torch.nn.Linear(dim, len(levels))
+        self.project_out = torch.nn.Linear(len(levels), dim)
+
+    def forward(self, x):
+        from oracle.condenc_oracle import fsq_quantize
+        codes, idx = fsq_quantize(self.project_in(x))
+        return self.project_out(codes), idx.unsqueeze(-1)
+
+
+def gen_tokenizer(name, dtype, seed):
+    """AttentionPooler (base:734-859), AceStepAudioTokenizer (base:1181-1223, with
+    the restated FSQ) and AudioTokenDetokenizer (base:862-994) of the reference."""
+    from acehip.weights import synth_tokenizer_weights
+    C, M = _import_ref("base")
+    M.ResidualFSQ = _FsqRestated
+    cfg = condenc_config("tiny")
+    rc = ref_config(C, cfg, num_lyric_encoder_hidden_layers=cfg.num_lyric_encoder_hidden_layers,
+                    num_timbre_encoder_hidden_layers=cfg.num_timbre_encoder_hidden_layers,
+                    num_attention_pooler_hidden_layers=cfg.num_attention_pooler_hidden_layers, fsq_dim=cfg.hidden_size)
+    W = synth_tokenizer_weights(cfg, seed=seed, mode="parity")
+    tok = M.AceStepAudioTokenizer(rc).eval()
+    det = M.AudioTokenDetokenizer(rc).eval()
+    mt, ut = tok.load_state_dict({k[len("tokenizer."):]: v for k, v in W.items() if k.startswith("tokenizer.")},
+                                 strict=False)
+    md, ud = det.load_state_dict({k[len("detokenizer."):]: v for k, v in W.items() if k.startswith("detokenizer.")},
+                                 strict=False)
+    assert not ut and not ud and all("rotary" in k for k in mt + md), (mt, ut, md, ud)
+    tok, det = tok.to(dtype), det.to(dtype)
+    g = torch.Generator().manual_seed(seed + 1)
+    N, T = 2, 30
+    x = torch.randn(N, T, cfg.audio_acoustic_hidden_dim, generator=g).to(dtype)
+    pooled_in = torch.randn(N, T // 5, 5, cfg.hidden_size, generator=g).to(dtype)
+    det_in = torch.randn(N, T // 5, cfg.hidden_size, generator=g).to(dtype)
+    with torch.no_grad():
+        pooled = tok.attention_pooler(pooled_in)
+        quant, idx = tok.tokenize(x)
+        det_out = det(det_in)
+        hints = det(quant)
+    save_file({"x": x, "pooled_in": pooled_in, "pooled": pooled.contiguous(), "quantized": quant.contiguous(),
+               "indices": idx.contiguous(), "det_in": det_in, "det_out": det_out.contiguous(),
+               "hints": hints.contiguous()}, os.path.join(OUT, f"tokenizer_{name}.safetensors"))
+    return {"cfg": cfg.__dict__, "dtype": str(dtype), "seed": seed, "weights_checksum": checksum(W),
+            "note": "ResidualFSQ replaced by the oracle restatement (vector_quantize_pytorch absent): quantizer parity unpinned"}
+
+
 def main_only(which):
     """Add fixtures to an existing manifest without regenerating the rest."""
     torch.set_num_threads(8)
@@ -266,6 +319,9 @@ def main_only(which):
         manifest["sampler"]["base_s8_adg"] = gen_sampler("base", "base_s8_adg", bf, 1, 40, infer_steps=8,
                                                          shift=3.0, diffusion_guidance_sale=7.0,
                                                          use_adg=True)
+    if "tokenizer" in which:
+        manifest["tokenizer"] = {f"tiny_{str(dt).split('.')[-1]}": gen_tokenizer(f"tiny_{str(dt).split('.')[-1]}", dt, 41)
+                                 for dt in (torch.float32, torch.bfloat16)}
     if "condenc" in which:
         ce = {}
         for width in ("tiny", "full"):
