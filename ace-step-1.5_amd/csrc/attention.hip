@@ -42,6 +42,9 @@ namespace {
 #ifndef ATT_DEFER
 #define ATT_DEFER 0        // second head's waves run P·V one tile late (SIMD-partner stagger;
 #endif                     // measured neutral-to-negative on MI355X, kept as an A/B switch)
+#ifndef ATT_XCD
+#define ATT_XCD 1          // XCD-aware block → work-unit remap
+#endif
 #ifndef ATT_PRIO
 #define ATT_PRIO 1         // static s_setprio 1 for the deferred (younger) half
 #endif
@@ -88,7 +91,11 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const int r = lane & 31, hh = lane >> 5;
     // work unit u = (b, kvh, q-block), q-block fastest; blocks past sp.full are the
     // KV-range parts of the tail units (tail balancing, see attention())
+    // XCD-aware: the blocks one XCD receives (bid ≡ x mod 8) take a contiguous unit range,
+    // so the q-blocks of one (b, kv head) share that XCD's L2 copy of its K/V tiles
+    // (whole units only: the tail-split parts must stay the grid's last blocks)
     int u = blockIdx.x, part = 0, nsplit = 1;
+    if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
     if (u >= sp.full) {
         const int j = u - sp.full;
         u = sp.full + j / sp.nsplit;
