@@ -48,6 +48,81 @@ __device__ __forceinline__ void ring_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Epilogue of one wave's SM×SN grid of 16×16 sub-tiles: lane (fr, fc) holds row
+// row0 + 16i + fr, columns col0 + 16j + 4fc .. +3 (the transposed MFMA tile).
+// Adjacent sub-tiles j, j+1 are paired and the lane pair (fc, fc ^ 1) swaps four
+// accumulators (lane ^ 16), so every lane owns 8 CONTIGUOUS columns of one
+// sub-tile: one 16-B load / store per operand instead of two 8-B ones (the
+// epilogue is store-issue-bound, MI355X_MICROARCH "attention epilogue store
+// tail").  SwiGLU: the wave's columns are whole 64-column panels [32 gate | 32 up].
+__device__ __forceinline__ void pair8(const f32x4 &lo, const f32x4 &hi, bool odd, float (&v)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float got = __shfl_xor(odd ? lo[r] : hi[r], 16, 64);
+        v[r] = odd ? got : lo[r];
+        v[4 + r] = odd ? hi[r] : got;
+    }
+}
+
+template <int SM, int SN, int EPI>
+__device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&acc)[SM][SN], int row0, int col0,
+                                              int fr, int fc) {
+    static_assert(SN % 2 == 0, "sub-tiles are paired");
+    const bool odd = fc & 1;
+    const int cpos = (fc >> 1) * 8;          // this lane's 8-column group inside its sub-tile
+#pragma unroll
+    for (int i = 0; i < SM; ++i) {
+        const int m = row0 + i * 16 + fr;
+        const bool live = m < a.M;           // rows past M still join the lane exchange
+        if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+            for (int pnl = 0; pnl < SN / 4; ++pnl) {
+                // silu(gate)·up in the MFMA layout first, then one exchange of the products
+                f32x4 p0, p1;
+                float o[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    p0[r] = rbf(silu_f(rbf(acc[i][4 * pnl][r]))) * rbf(acc[i][4 * pnl + 2][r]);
+                    p1[r] = rbf(silu_f(rbf(acc[i][4 * pnl + 1][r]))) * rbf(acc[i][4 * pnl + 3][r]);
+                }
+                pair8(p0, p1, odd, o);
+                const int nout = ((col0 + pnl * 64) >> 1) + (odd ? 16 : 0) + cpos;
+                if (live) *(uint4 *)(a.C + (int64_t)m * a.ldc + nout) = pack8(o);
+            }
+        } else {
+            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
+#pragma unroll
+            for (int jp = 0; jp < SN / 2; ++jp) {
+                float o[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
+                if (!live) continue;
+                if constexpr (EPI == EPI_STORE) {
+                    if (a.bias) {
+                        float bb[8];
+                        unpack8(*(const uint4 *)(a.bias + n), bb);
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                    }
+                } else {
+                    float rr[8];
+                    unpack8(*(const uint4 *)(a.res + (int64_t)m * a.ldr + n), rr);
+                    if constexpr (EPI == EPI_GATED_RES) {
+                        float gg[8];
+                        unpack8(*(const uint4 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(rbf(o[r]) * gg[r]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(o[r]);
+                    }
+                }
+                *(uint4 *)(a.C + (int64_t)m * a.ldc + n) = pack8(o);
+            }
+        }
+    }
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
 __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     constexpr int NW = WM * WN;
@@ -122,110 +197,7 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
         }
     }
 
-    // epilogue: lane owns row m, columns n..n+3 of each 16x16 sub-tile
-#pragma unroll
-    for (int i = 0; i < SM; ++i) {
-        const int m = m0 + wm * TM + i * 16 + fr;
-        if (m >= a.M) continue;
-        if constexpr (EPI == EPI_SWIGLU) {
-            // packed rows: within each 64-row panel, rows [0,32) gate, [32,64) up
-#pragma unroll
-            for (int pnl = 0; pnl < TN / 64; ++pnl)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int nout = ((n0 + wn * TN + pnl * 64) >> 1) + j * 16 + fc * 4;
-                    float o[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float g = rbf(acc[i][4 * pnl + j][r]);
-                        const float u = rbf(acc[i][4 * pnl + j + 2][r]);
-                        o[r] = rbf(silu_f(g)) * u;
-                    }
-                    *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
-                }
-        } else {
-            const int b = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
-#pragma unroll
-            for (int j = 0; j < SN; ++j) {
-                const int n = n0 + wn * TN + j * 16 + fc * 4;
-                float o[4];
-                if constexpr (EPI == EPI_STORE) {
-                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
-                    if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + bb[r];
-                } else {
-                    float rr[4];
-                    unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + n), rr);
-                    if constexpr (EPI == EPI_GATED_RES) {
-                        float gg[4];
-                        unpack4(*(const uint2 *)(a.gate + (int64_t)b * a.gate_bstride + n), gg);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[i][j][r]) * gg[r]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[i][j][r]);
-                    }
-                }
-                *(uint2 *)(a.C + (int64_t)m * a.ldc + n) = pack4(o);
-            }
-        }
-    }
-}
-
-// Epilogue of one wave's SM×SN grid of 16×16 sub-tiles: lane (fr, fc) owns row
-// row0 + 16i + fr and columns col0 + 16j + 4fc .. +3 (the transposed MFMA tile).
-// SwiGLU: the wave's columns are whole 64-column panels [32 gate | 32 up].
-template <int SM, int SN, int EPI>
-__device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&acc)[SM][SN], int row0, int col0,
-                                              int fr, int fc) {
-#pragma unroll
-    for (int i = 0; i < SM; ++i) {
-        const int m = row0 + i * 16 + fr;
-        if (m >= a.M) continue;
-        if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-            for (int pnl = 0; pnl < SN / 4; ++pnl)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int nout = ((col0 + pnl * 64) >> 1) + j * 16 + fc * 4;
-                    float o[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float g = rbf(acc[i][4 * pnl + j][r]);
-                        const float u = rbf(acc[i][4 * pnl + j + 2][r]);
-                        o[r] = rbf(silu_f(g)) * u;
-                    }
-                    *(uint2 *)(a.C + (int64_t)m * a.ldc + nout) = pack4(o);
-                }
-        } else {
-            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
-#pragma unroll
-            for (int j = 0; j < SN; ++j) {
-                const int n = col0 + j * 16 + fc * 4;
-                float o[4];
-                if constexpr (EPI == EPI_STORE) {
-                    float bb[4] = {0.f, 0.f, 0.f, 0.f};
-                    if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + bb[r];
-                } else {
-                    float rr[4];
-                    unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + n), rr);
-                    if constexpr (EPI == EPI_GATED_RES) {
-                        float gg[4];
-                        unpack4(*(const uint2 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[i][j][r]) * gg[r]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[i][j][r]);
-                    }
-                }
-                *(uint2 *)(a.C + (int64_t)m * a.ldc + n) = pack4(o);
-            }
-        }
-    }
+    epilogue_tile<SM, SN, EPI>(a, acc, m0 + wm * TM, n0 + wn * TN, fr, fc);
 }
 
 // ---------------------------------------------------------------------------
