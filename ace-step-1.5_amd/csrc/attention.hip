@@ -323,18 +323,25 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         if (tid == 0) sp.cnt[u - sp.full] = 0;         // self-resetting for the next launch
     }
 
-    if (qi >= Sq) return;
+    if (qi >= Sq) return;                     // both lanes of a row pair (lane, lane ^ 32) leave together
     const float inv = 1.0f / l;
     bf16_t *op = o + ((int64_t)b * Sq + qi) * o_ld + hq * 128;
+    // lane (r, hh) holds columns 32dt + 8gg + 4hh .. +3 of its row; the two half-waves swap one
+    // 4-column group per pair (gg, gg+1) so each lane stores 8 contiguous columns as one 16-B
+    // store (the store tail is issue-bound: MI355X_MICROARCH "attention epilogue store tail")
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-            const int d = 32 * dt + 8 * gg + 4 * hh;
-            float ov[4];
+        for (int gp = 0; gp < 2; ++gp) {
+            float v[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ov[j] = oacc[dt][4 * gg + j] * inv;
-            *(uint2 *)(op + d) = pack4(ov);
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = oacc[dt][8 * gp + j] * inv, a1 = oacc[dt][8 * gp + 4 + j] * inv;
+                const float got = __shfl_xor(hh ? a0 : a1, 32, 64);
+                v[j] = hh ? got : a0;
+                v[4 + j] = hh ? a1 : got;
+            }
+            *(uint4 *)(op + 32 * dt + 16 * gp + 8 * hh) = pack8(v);
         }
 }
 
