@@ -64,6 +64,20 @@ __device__ __forceinline__ void unpack4(const uint2 &u, float *f) {
     f[2] = bf2f((bf16_t)(u.y & 0xffff)); f[3] = bf2f((bf16_t)(u.y >> 16));
 }
 
+// 16×16 MFMA output tiles (transposed layout: lane (fr = lane & 15, fc = lane >> 4) holds
+// row fr, columns 4fc..4fc+3): pair sub-tiles lo (cols c..c+15) and hi (c+16..c+31) so
+// that lane (fr, fc) ends up with 8 CONTIGUOUS columns — of lo if fc is even, of hi if odd —
+// at offset 8·(fc >> 1): one 4-value swap with lane ^ 16.  Turns an epilogue's 8-B
+// accesses into 16-B ones (the store tail is issue-bound).
+__device__ __forceinline__ void pair8(const f32x4 &lo, const f32x4 &hi, bool odd, float (&v)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float got = __shfl_xor(odd ? lo[r] : hi[r], 16, 64);
+        v[r] = odd ? got : lo[r];
+        v[4 + r] = odd ? hi[r] : got;
+    }
+}
+
 // ------------------------------------------------------- wave reductions ---
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

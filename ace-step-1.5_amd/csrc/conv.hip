@@ -47,6 +47,16 @@ __device__ __forceinline__ float snake1(float x, float a, float ib) {
     return x + ib * s * s;
 }
 
+// snake1 over 8 channels with 16-B parameter loads (sa / sib fp32 per channel)
+__device__ __forceinline__ void snake8(const float (&x)[8], const float *sa, const float *sib, float (&y)[8]) {
+    const float4 a0 = *(const float4 *)sa, a1 = *(const float4 *)(sa + 4);
+    const float4 b0 = *(const float4 *)sib, b1 = *(const float4 *)(sib + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) y[r] = snake1(x[r], av[r], bv[r]);
+}
+
 // Both operands by global_load_lds into a 2-stage ring: [A im2col rows | W rows],
 // 128-B rows, XOR-swizzled on the source address (as gemm.hip).
 struct ConvTile {
@@ -118,31 +128,38 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         }
     }
 
+    // epilogue: sub-tiles paired by a lane exchange (pair8) → 8 contiguous channels per lane,
+    // 16-B loads / stores (the store tail is issue-bound); partners (lane ^ 16) share the row
+    const bool odd = fc & 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int64_t m = m0 + wm * 64 + i * 16 + fr;
         const int64_t row = m * a.c_stride + a.c_off + phase;
         if (m >= a.M || row < 0 || row >= a.L_out) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + wn * 64 + j * 16 + fc * 4;
-            float bb[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
-            if (a.bias) unpack4(*(const uint2 *)(a.bias + n), bb);
+        for (int jp = 0; jp < 2; ++jp) {
+            float o[8];
+            pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+            const int n = n0 + wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
+            if (a.bias) {
+                float bb[8];
+                unpack8(*(const uint4 *)(a.bias + n), bb);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = rbf(acc[i][j][r] + bb[r]);   // conv output (bf16)
-            if constexpr (RES) {
-                float rr[4];
-                unpack4(*(const uint2 *)(a.res + row * a.N + n), rr);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = rbf(rr[r] + o[r]);
+                for (int r = 0; r < 8; ++r) o[r] += bb[r];
             }
-            if constexpr (RAW) *(uint2 *)(a.out + row * a.N + n) = pack4(o);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) o[r] = rbf(o[r]);                    // conv output (bf16)
+            if constexpr (RES) {
+                float rr[8];
+                unpack8(*(const uint4 *)(a.res + row * a.N + n), rr);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + o[r]);
+            }
+            if constexpr (RAW) *(uint4 *)(a.out + row * a.N + n) = pack8(o);
             if constexpr (SN) {
-                const float4 sa = *(const float4 *)(a.sa + n);
-                const float4 sb = *(const float4 *)(a.sib + n);
-                const float sn[4] = {snake1(o[0], sa.x, sb.x), snake1(o[1], sa.y, sb.y),
-                                     snake1(o[2], sa.z, sb.z), snake1(o[3], sa.w, sb.w)};
-                *(uint2 *)(a.out_s + row * a.N + n) = pack4(sn);
+                float sn[8];
+                snake8(o, a.sa + n, a.sib + n, sn);
+                *(uint4 *)(a.out_s + row * a.N + n) = pack8(sn);
             }
         }
     }
@@ -263,24 +280,24 @@ __global__ __launch_bounds__(256, 2) void resunit128_kernel(ResUnitArgs u) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
         }
     // epilogue 2: x' = x + bf16(acc + b2); raw (optional) + snake_next
+    const bool odd = fc & 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int64_t m = m0 + wm * 64 + i * 16 + fr;
         if (m >= a.M) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = wn * 64 + j * 16 + fc * 4;
-            float bb[4], rr[4], o[4];
-            unpack4(*(const uint2 *)(u.b2 + n), bb);
-            unpack4(*(const uint2 *)(u.x + m * 128 + n), rr);
+        for (int jp = 0; jp < 2; ++jp) {
+            float o[8], bb[8], rr[8];
+            pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+            const int n = wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
+            unpack8(*(const uint4 *)(u.b2 + n), bb);
+            unpack8(*(const uint4 *)(u.x + m * 128 + n), rr);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = rbf(rr[r] + rbf(acc[i][j][r] + bb[r]));
-            if constexpr (RAW) *(uint2 *)(u.x + m * 128 + n) = pack4(o);
-            const float4 sa = *(const float4 *)(u.sa_next + n);
-            const float4 sb = *(const float4 *)(u.sib_next + n);
-            const float sn[4] = {snake1(o[0], sa.x, sb.x), snake1(o[1], sa.y, sb.y),
-                                 snake1(o[2], sa.z, sb.z), snake1(o[3], sa.w, sb.w)};
-            *(uint2 *)(u.out_s + m * 128 + n) = pack4(sn);
+            for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+            if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
+            float sn[8];
+            snake8(o, u.sa_next + n, u.sib_next + n, sn);
+            *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
         }
     }
 }

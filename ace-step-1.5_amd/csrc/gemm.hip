@@ -55,15 +55,6 @@ __device__ __forceinline__ void ring_barrier() {
 // sub-tile: one 16-B load / store per operand instead of two 8-B ones (the
 // epilogue is store-issue-bound, MI355X_MICROARCH "attention epilogue store
 // tail").  SwiGLU: the wave's columns are whole 64-column panels [32 gate | 32 up].
-__device__ __forceinline__ void pair8(const f32x4 &lo, const f32x4 &hi, bool odd, float (&v)[8]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float got = __shfl_xor(odd ? lo[r] : hi[r], 16, 64);
-        v[r] = odd ? got : lo[r];
-        v[4 + r] = odd ? hi[r] : got;
-    }
-}
-
 template <int SM, int SN, int EPI>
 __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&acc)[SM][SN], int row0, int col0,
                                               int fr, int fc) {
