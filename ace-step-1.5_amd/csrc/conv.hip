@@ -310,24 +310,22 @@ template <int COUT>
 __global__ __launch_bounds__(256) void conv_out_kernel(const bf16_t *__restrict__ in, int64_t L, int Cin,
                                                        const float *__restrict__ w,  // [COUT][7][Cin]
                                                        float *__restrict__ out) {
+    // the halo window stays position-major ([262][Cin], 16-B chunks XOR-swizzled by the row so
+    // the per-lane row reads of one chunk spread over all banks): 16-B global loads and 16-B
+    // LDS writes (the former channel-major transpose was 2-B LDS stores, 700 GB/s)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int P = 256 + 6;
-    bf16_t *xs = (bf16_t *)smem;   // [Cin][P]
-    float *ws = (float *)(smem + ((size_t)Cin * P * 2 + 15) / 16 * 16);
+    const int chunks = Cin / 8, cm = chunks - 1;
+    char *xs = smem;                                   // [P][Cin] bf16, swizzled chunks
+    float *ws = (float *)(smem + (size_t)P * Cin * 2);
     const int64_t t0 = (int64_t)blockIdx.x * 256;
     for (int i = threadIdx.x; i < COUT * 7 * Cin; i += 256) ws[i] = w[i];
-    const int chunks = Cin / 8;
     for (int c = threadIdx.x; c < P * chunks; c += 256) {
         const int p = c / chunks, ch = c % chunks;
         const int64_t pos = t0 - 3 + p;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (pos >= 0 && pos < L) v = *(const uint4 *)(in + pos * Cin + ch * 8);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            xs[(ch * 8 + 2 * j) * P + p] = (bf16_t)(wv[j] & 0xffff);
-            xs[(ch * 8 + 2 * j + 1) * P + p] = (bf16_t)(wv[j] >> 16);
-        }
+        *(uint4 *)(xs + (size_t)p * Cin * 2 + ((ch ^ (p & cm)) << 4)) = v;
     }
     __syncthreads();
     const int64_t t = t0 + threadIdx.x;
@@ -335,13 +333,17 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const bf16_t *__restrict_
     float acc[COUT];
 #pragma unroll
     for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
-    for (int c = 0; c < Cin; ++c) {
-        const bf16_t *xr = xs + c * P + threadIdx.x;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const float x = bf2f(xr[k]);
+    for (int k = 0; k < 7; ++k) {
+        const int row = threadIdx.x + k;
+        const char *xr = xs + (size_t)row * Cin * 2;
+        for (int c = 0; c < chunks; ++c) {
+            float x[8];
+            unpack8(*(const uint4 *)(xr + ((c ^ (row & cm)) << 4)), x);
 #pragma unroll
-            for (int o = 0; o < COUT; ++o) acc[o] += x * ws[(o * 7 + k) * Cin + c];
+            for (int e = 0; e < 8; ++e)
+#pragma unroll
+                for (int o = 0; o < COUT; ++o) acc[o] += x[e] * ws[(o * 7 + k) * Cin + c * 8 + e];
         }
     }
 #pragma unroll
@@ -512,7 +514,8 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
 }
 
 int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s) {
-    if (Cout != 2 || Cin % 8) return fail(-1, "conv_out: Cout must be 2, Cin%8 == 0");
+    if (Cout != 2 || Cin % 8 || ((Cin / 8) & (Cin / 8 - 1)))
+        return fail(-1, "conv_out: Cout must be 2, Cin/8 a power of two");
     const size_t smem = ((size_t)Cin * 262 * 2 + 15) / 16 * 16 + (size_t)2 * 7 * Cin * 4;
     conv_out_kernel<2><<<(unsigned)((L + 255) / 256), 256, smem, s>>>(in_s, L, Cin, w, out);
     HIP_TRY(hipGetLastError());
