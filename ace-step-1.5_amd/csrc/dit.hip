@@ -73,6 +73,7 @@ struct acehip_dit {
     int uniform_from = 1 << 30;
     bf16_t *cnull = nullptr, *vnull = nullptr;   // [L][D], [q_dim]
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
+    void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs (short songs / turbo)
     size_t tmp_elems = 0;
 
     // optional per-kernel event timing (acehip_dit_profile)
@@ -83,6 +84,13 @@ struct acehip_dit {
     std::vector<int> ev_kind;          // kind of each recorded pair
     int ev_used = 0;
 };
+
+// every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
+static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
+    g.ws = h->gemm_ws;
+    g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
+    return gemm(g, s);
+}
 
 namespace {
 
@@ -254,6 +262,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
+    h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
     h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
     h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
@@ -418,14 +427,14 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
     GemmArgs g{};
     g.A = (const bf16_t *)enc; g.lda = D; g.W = h->wce; g.ldw = D; g.C = h->E; g.ldc = D;
     g.M = M; g.N = D; g.K = D; g.epi = EPI_STORE; g.bias = h->bce;
-    int rc = gemm(g, s);
+    int rc = hgemm(h, g, s);
     if (rc) return rc;
     const size_t per = (size_t)Bc * kvd * Lenc;
     for (int l = 0; l < h->L; ++l) {
         GemmArgs k{};
         k.A = h->E; k.lda = D; k.W = h->layers[l].wckv; k.ldw = D; k.C = h->KVtmp; k.ldc = 2 * kvd;
         k.M = M; k.N = 2 * kvd; k.K = D; k.epi = EPI_STORE;
-        if ((rc = gemm(k, s))) return rc;
+        if ((rc = hgemm(h, k, s))) return rc;
         HeadPostArgs p{};
         p.src = h->KVtmp; p.ld_src = 2 * kvd; p.B = Bc; p.S = Lenc;
         p.nq = 0; p.nk = h->cfg.kv_heads; p.nv = h->cfg.kv_heads;
@@ -459,7 +468,7 @@ int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream) {
         GemmArgs g{};
         g.A = h->vnull; g.lda = qd; g.W = h->layers[l].wco; g.ldw = qd; g.C = h->cnull + (size_t)l * D; g.ldc = D;
         g.M = 1; g.N = D; g.K = qd; g.epi = EPI_STORE;
-        if ((rc = gemm(g, s))) return rc;
+        if ((rc = hgemm(h, g, s))) return rc;
     }
     h->uniform_from = first_row;
     return 0;
@@ -496,7 +505,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     GemmArgs g{};
     g.A = h->Xin; g.lda = 384; g.W = h->win; g.ldw = 384; g.C = h->X; g.ldc = D;
     g.M = M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
-    RUN(gemm(g, s));
+    RUN(hgemm(h, g, s));
 
     const size_t cper = (size_t)Bc * kvd * Le;
     const int Bq = std::min(h->uniform_from, Bc), Mq = Bq * S;   // rows with a real cross-attention
@@ -513,7 +522,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         q.hp.B = Bc; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
-        RUN(timed(h, 2, s, [&] { return gemm(q, s); }));
+        RUN(timed(h, 2, s, [&] { return hgemm(h, q, s); }));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
             return attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
                              scale, qd, h->attn_ws, s);
@@ -522,7 +531,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
-        RUN(timed(h, 3, s, [&] { return gemm(o, s); }));
+        RUN(timed(h, 3, s, [&] { return hgemm(h, o, s); }));
         // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
         // rows, base:1907) get their constant cross-O output cnull[l] (set_uniform_rows)
         RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, Mq, D, eps, s));
@@ -531,7 +540,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         cq.M = Mq; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
         cq.hp.B = Bq; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
         cq.hp.eps = eps;
-        RUN(gemm(cq, s));
+        RUN(hgemm(h, cq, s));
         RUN(timed(h, 6, s, [&] {
             return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bq, H, KV, S, Le, -1, scale, qd,
                              h->attn_ws, s);
@@ -539,19 +548,19 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         GemmArgs co{};
         co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
         co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
-        RUN(timed(h, 3, s, [&] { return gemm(co, s); }));
+        RUN(timed(h, 3, s, [&] { return hgemm(h, co, s); }));
         if (Mq < M) RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533)
         RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s));
         GemmArgs gu{};
         gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
         gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;
-        RUN(timed(h, 0, s, [&] { return gemm(gu, s); }));
+        RUN(timed(h, 0, s, [&] { return hgemm(h, gu, s); }));
         GemmArgs dn{};
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
-        RUN(timed(h, 1, s, [&] { return gemm(dn, s); }));
+        RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s); }));
     }
     // norm_out AdaLN + proj_out (base:1491-1501)
     RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s));
@@ -559,7 +568,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     po.A = h->XN; po.lda = D; po.W = h->wout; po.ldw = D;
     po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
     po.M = M; po.N = 128; po.K = D; po.epi = EPI_STORE; po.bias = h->bout;
-    RUN(gemm(po, s));
+    RUN(hgemm(h, po, s));
     if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
 #undef RUN
     return 0;
@@ -639,6 +648,16 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
     return gemm(g, (hipStream_t)stream);
 }
 
+// lazily allocated split-K workspace of the standalone kernel entry points (one per device)
+static void *abi_gemm_ws() {
+    static std::map<int, void *> by_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    void *&ws = by_dev[dev];
+    if (!ws && hipMalloc(&ws, GEMM_WS_BYTES) != hipSuccess) ws = nullptr;
+    return ws;
+}
+
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,
                         int K, const void *bias, int epi, int variant, void *stream) {
     GemmArgs g{};
@@ -650,6 +669,12 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
     else if (epi == 0) g.epi = EPI_STORE;
     else return fail(ACEHIP_E_ARG, "gemm_ex: epilogue");
     if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
+    if (variant < 0) {   // production dispatch incl. split-K for small grids
+        g.ws = abi_gemm_ws();
+        g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
+        if (epi == 2) g.ldr = ldc;
+        return gemm(g, (hipStream_t)stream);
+    }
     return gemm_variant(g, variant, (hipStream_t)stream);
 }
 
@@ -679,6 +704,8 @@ int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int 
     g.hp.qw = (const bf16_t *)qw; g.hp.kw = (const bf16_t *)kw;
     g.hp.cos = (const bf16_t *)cos; g.hp.sin = (const bf16_t *)sin;
     g.hp.q = (bf16_t *)q; g.hp.k = (bf16_t *)k; g.hp.v = (bf16_t *)v; g.hp.S_dst = S; g.hp.eps = eps;
+    g.ws = abi_gemm_ws();
+    g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
     return gemm(g, (hipStream_t)stream);
 }
 

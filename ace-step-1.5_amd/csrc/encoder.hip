@@ -50,7 +50,15 @@ struct acehip_enc {
     // workspace
     bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *O128;
     void *attn_ws = nullptr;
+    void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs
 };
+
+// every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
+static inline int hgemm(acehip_enc *h, GemmArgs g, hipStream_t s) {
+    g.ws = h->gemm_ws;
+    g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
+    return gemm(g, s);
+}
 
 namespace {
 
@@ -162,6 +170,7 @@ int acehip_enc_create(int device, const acehip_enc_cfg *cfg, acehip_enc **out) {
     h->Qh = A(M * qd); h->Kh = A(M * kvd); h->Vh = A(M * kvd); h->AO = A(M * qd);
     h->Hb = A(M * F);
     h->O128 = cfg->out_dim ? A(M * 128) : nullptr;
+    h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->rope_cos = A((size_t)cfg->max_S * 128); h->rope_sin = A((size_t)cfg->max_S * 128);
     if (ok) {
         const size_t wb = attention_ws_bytes();
@@ -267,22 +276,22 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
         q.hp.B = B; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
-        RUN(gemm(q, s));
+        RUN(hgemm(h, q, s));
         RUN(attention(h->Qh, h->Kh, h->Vh, h->AO, B, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1, scale, qd,
                       h->attn_ws, s, kmask));
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_RES; o.res = h->X; o.ldr = D;
-        RUN(gemm(o, s));
+        RUN(hgemm(h, o, s));
         RUN(rmsnorm_mod(h->X, ly.ln2, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
         GemmArgs gu{};
         gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
         gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;
-        RUN(gemm(gu, s));
+        RUN(hgemm(h, gu, s));
         GemmArgs dn{};
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_RES; dn.res = h->X; dn.ldr = D;
-        RUN(gemm(dn, s));
+        RUN(hgemm(h, dn, s));
     }
     if (!h->cfg.out_dim) {
         RUN(rmsnorm_mod(h->X, h->norm, nullptr, nullptr, 0, S, (bf16_t *)out, M, D, eps, s));
@@ -293,7 +302,7 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
     GemmArgs po{};
     po.A = h->XN; po.lda = D; po.W = h->wout; po.ldw = D; po.C = h->O128; po.ldc = 128;
     po.M = M; po.N = 128; po.K = D; po.epi = EPI_STORE; po.bias = h->bout;
-    RUN(gemm(po, s));
+    RUN(hgemm(h, po, s));
     RUN(copy_cols(h->O128, 128, (bf16_t *)out, h->cfg.out_dim, M, h->cfg.out_dim, s));
 #undef RUN
     return 0;

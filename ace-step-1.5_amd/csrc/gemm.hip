@@ -126,6 +126,8 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     static_assert(NINS % NW == 0, "staging must split evenly over waves");
     static_assert(EPI != EPI_SWIGLU || TN % 64 == 0, "SwiGLU pairs 32+32 columns per 64-column panel");
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
+    // split-K (EPI_PARTIAL): split blockIdx.y covers K-tiles [y·kper, min(nk, (y+1)·kper))
+    const int ktile0 = EPI == EPI_PARTIAL ? (int)blockIdx.y * a.kper : 0;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
@@ -146,8 +148,8 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
         const int q = wave + NW * i;
         const int r = q * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
-        if (r < BM) src[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8;
-        else src[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8;
+        if (r < BM) src[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8 + ktile0 * BK;
+        else src[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8 + ktile0 * BK;
     }
     auto stage = [&](int buf, int k0) {
         char *b = lds + buf * STAGE;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < SN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = a.K / BK;
+    const int nk = EPI == EPI_PARTIAL ? min(a.kper, a.K / BK - ktile0) : a.K / BK;
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
         if (s < nk) stage(s, s * BK);
@@ -188,7 +190,66 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
         }
     }
 
-    epilogue_tile<SM, SN, EPI>(a, acc, m0 + wm * TM, n0 + wn * TN, fr, fc);
+    if constexpr (EPI == EPI_PARTIAL) {
+        // fp32 partial sums of this split: lane's 4 consecutive columns → one 16-B store
+        float *ws = (float *)a.ws + (size_t)blockIdx.y * a.M * a.N;
+#pragma unroll
+        for (int i = 0; i < SM; ++i) {
+            const int m = m0 + wm * TM + i * 16 + fr;
+            if (m >= a.M) continue;
+#pragma unroll
+            for (int j = 0; j < SN; ++j)
+                *(f32x4 *)(ws + (int64_t)m * a.N + n0 + wn * TN + j * 16 + fc * 4) = acc[i][j];
+        }
+        return;
+    } else {
+        epilogue_tile<SM, SN, EPI>(a, acc, m0 + wm * TM, n0 + wn * TN, fr, fc);
+    }
+}
+
+// Split-K reduction + the GEMM's epilogue (same rounding as epilogue_tile): the
+// splits are summed in order (deterministic); one thread per 4 output columns.
+// SwiGLU: packed columns p·64 + [0, 32) gate, p·64 + [32, 64) up → output p·32 + i.
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a, int splits, bf16_t *out, int64_t ldo) {
+    const int nout = a.epi == EPI_SWIGLU ? a.N / 2 : a.N;
+    const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (e >= (int64_t)a.M * nout) return;
+    const int m = (int)(e / nout), q = (int)(e % nout);
+    const float *ws = (const float *)a.ws;
+    const size_t plane = (size_t)a.M * a.N;
+    auto sum4 = [&](int col) {
+        f32x4 t = *(const f32x4 *)(ws + (int64_t)m * a.N + col);
+        for (int sp = 1; sp < splits; ++sp) t += *(const f32x4 *)(ws + sp * plane + (int64_t)m * a.N + col);
+        return t;
+    };
+    float o[4];
+    if (a.epi == EPI_SWIGLU) {
+        const int pnl = q / 32, i = q % 32;
+        const f32x4 g = sum4(pnl * 64 + i), u = sum4(pnl * 64 + 32 + i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = rbf(silu_f(rbf(g[r]))) * rbf(u[r]);
+    } else {
+        const f32x4 acc = sum4(q);
+        if (a.epi == EPI_STORE || a.epi == EPI_HEADPOST) {
+            float bb[4] = {0.f, 0.f, 0.f, 0.f};
+            if (a.bias && a.epi == EPI_STORE) unpack4(*(const uint2 *)(a.bias + q), bb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = acc[r] + bb[r];
+        } else {
+            float rr[4];
+            unpack4(*(const uint2 *)(a.res + (int64_t)m * a.ldr + q), rr);
+            if (a.epi == EPI_GATED_RES) {
+                float gg[4];
+                unpack4(*(const uint2 *)(a.gate + (int64_t)(m / a.rows_per_batch) * a.gate_bstride + q), gg);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(rbf(acc[r]) * gg[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = rr[r] + rbf(acc[r]);
+            }
+        }
+    }
+    *(uint2 *)(out + (int64_t)m * ldo + q) = pack4(o);
 }
 
 // ---------------------------------------------------------------------------
@@ -594,8 +655,50 @@ int gemm_pick_variant(int64_t M, int N) {
     return c7 < c8 ? 7 : 8;
 }
 
+// Split-K for grids that cannot fill half the chip even with 128×128 tiles (short
+// songs / turbo: M = Bc·S of a few hundred rows): the K range is split so the grid
+// reaches ~1 block per CU, every split stores fp32 partials, and one launch sums
+// them in order and applies the epilogue (the head-post case then runs the
+// standalone head_post kernel on the staged bf16 projection).
+static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
+    GemmArgs p = a;
+    const int nk = a.K / BK;
+    p.kper = (nk + splits - 1) / splits;
+    splits = (nk + p.kper - 1) / p.kper;
+    const int tiles = ((a.M + 127) / 128) * (a.N / 128);
+    gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
+    HIP_TRY(hipGetLastError());
+    bf16_t *out = a.C;
+    int64_t ldo = a.ldc;
+    if (a.epi == EPI_HEADPOST) {   // bf16 projection staged after the partials
+        out = (bf16_t *)((char *)a.ws + (size_t)splits * a.M * a.N * 4);
+        ldo = a.N;
+    }
+    const int nout = a.epi == EPI_SWIGLU ? a.N / 2 : a.N;
+    const int64_t thr = (int64_t)a.M * nout / 4;
+    splitk_epilogue_kernel<<<(unsigned)((thr + 255) / 256), 256, 0, s>>>(p, splits, out, ldo);
+    HIP_TRY(hipGetLastError());
+    if (a.epi == EPI_HEADPOST) {
+        HeadPostArgs h = a.hp;
+        h.src = out;
+        h.ld_src = a.N;
+        return head_post(h, s);
+    }
+    return 0;
+}
+
 int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.M <= 0) return 0;
+    if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
+        const int cus = num_cus();
+        const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
+        const int nk = a.K / BK;
+        if (tiles * 2 <= cus && nk >= 8) {
+            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4), (cus + tiles - 1) / tiles);
+            const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
+            if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s);
+        }
+    }
     if (a.N % 128 || a.K % BK || a.K <= 0)
         return fail(-1, "gemm: N%128 / K%64 violated (M=" + std::to_string(a.M) + " N=" +
                             std::to_string(a.N) + " K=" + std::to_string(a.K) + ")");

@@ -36,7 +36,13 @@ struct GemmArgs {
     const bf16_t *res; int64_t ldr; // residual (may alias C)
     const bf16_t *gate; int64_t gate_bstride; int rows_per_batch;
     HeadPostArgs hp;                // EPI_HEADPOST only (rows of hp.B·hp.S; hp.src/ld_src unused)
+    // split-K workspace (grids too small to fill the chip): fp32 partials [splits][M][N]
+    // + a bf16 [M][N] staging tile for the head-post case; null disables split-K
+    void *ws; size_t ws_bytes;
+    int kper;                       // internal: K-tiles per split (EPI_PARTIAL launches)
 };
+constexpr int EPI_PARTIAL = 5;
+constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace      // internal: store the fp32 accumulators of split blockIdx.y to ws
 int gemm(const GemmArgs &a, hipStream_t s);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
 

@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--no-condition", action="store_true",
                    help="feed synthetic encoder states directly (skip the HIP condition encoders)")
     p.add_argument("--lyric-len", type=int, default=512)
+    p.add_argument("--turbo", action="store_true",
+                   help="turbo sampler (table schedule, no CFG; SURVEY config 1 shape: --seconds 10 --infer-steps 8)")
     p.add_argument("--repaint", action="store_true",
                    help="SURVEY config 5: VAE encode of a synthetic 48 kHz stereo source -> DiT repaint of "
                         "[--repaint-start, --repaint-end) s -> VAE decode, all inside the timed song")
@@ -113,6 +115,8 @@ def main():
     S = (T + 1) // 2
     cfg = DiTConfig()
     vcfg = VAEConfig()
+    if args.turbo:
+        args.guidance = 1.0
     do_cfg = args.guidance > 1.0
     Bc = 2 if do_cfg else 1
 
@@ -128,7 +132,7 @@ def main():
         ce.load(synth_condenc_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch"))
         prep = HipPrepareCondition(ce)
         args.lenc = args.lyric_len + 1 + args.text_len
-    be = AceStepDiTBackend(rt, null, is_turbo=False, prepare_condition=prep)
+    be = AceStepDiTBackend(rt, null, is_turbo=args.turbo, prepare_condition=prep)
     vae = vae_w = None
     if not args.no_vae:
         vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=args.repaint, device=dev,
@@ -256,8 +260,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init weights of the real architecture, random conditioning)",
-        "config": {"workload": f"text2music {args.seconds:g}s, base/sft {args.infer_steps} steps, "
-                               f"shift {args.shift:g}, CFG {args.guidance:g} + APG, "
+        "config": {"workload": f"text2music {args.seconds:g}s, "
+                               + (f"turbo {args.infer_steps} steps (table, no CFG), " if args.turbo else
+                                  f"base/sft {args.infer_steps} steps, shift {args.shift:g}, CFG {args.guidance:g} + APG, ")
                                + ("DiT + VAE decode" if args.no_condition else "condition encoders + DiT + VAE decode")
                                + (f", repaint [{args.repaint_start:g}, {args.repaint_end:g}) s: VAE encode first"
                                   if args.repaint else ""),

@@ -272,7 +272,8 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
  * and tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
  * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage, 5: 256x256 2-stage,
  * 6: 192x256 2-stage, 7: 256x256 ping-pong, 8: 192x256 ping-pong; 3 and 5-8
- * need N % 256 == 0) — tuning and tests. */
+ * need N % 256 == 0; -1: the production choice, including split-K for grids
+ * that cannot fill half the chip) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 

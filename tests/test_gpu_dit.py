@@ -396,3 +396,33 @@ def test_weight_reload_matches_fresh_handle(gpu_device):
     torch.cuda.synchronize()
     assert torch.equal(va, vb)
     a.close(); b.close()
+
+
+@pytest.mark.parametrize("M,N,K", [(125, 2048, 6144), (125, 12288, 2048), (250, 4096, 2048), (61, 256, 1024)])
+def test_gemm_splitk_small_m(gpu_device, M, N, K):
+    """Split-K path for grids that cannot fill the chip (short songs / turbo): store,
+    residual and SwiGLU epilogues through the production dispatch (variant -1)."""
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(gpu_device, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(gpu_device, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    C = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, ff.ptr(b), EPI_STORE,
+                                          -1, ff.stream_ptr()))
+    torch.cuda.synchronize()
+    assert rel_l2(C.float().cpu(), (ref + b.float()).cpu()) < 5e-3
+    R = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
+    C2 = R.clone()
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C2), N, M, N, K, None, EPI_RES, -1,
+                                          ff.stream_ptr()))
+    torch.cuda.synchronize()
+    assert rel_l2(C2.float().cpu(), (R.float() + ref.bfloat16().float()).cpu()) < 5e-3
+    Cs = torch.empty(M, N // 2, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cs), N // 2, M, N, K, None,
+                                          EPI_SWIGLU, -1, ff.stream_ptr()))
+    torch.cuda.synchronize()
+    y = ref.bfloat16().float().view(M, N // 64, 2, 32)
+    gate, up = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
+    assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2

@@ -44,6 +44,7 @@ def _headpost_ref(C, B, S, nq, nk, nv, qw, kw, cos, sin, eps):
     (1, 77, 2, 1, 1, 128, True),       # tiny-config layout: one 256-col tile mixes k and v heads
     (2, 250, 4, 0, 0, 192, False),     # cross-attention Q: q heads only, no RoPE
     (3, 65, 2, 2, 4, 64, True),        # one K-tile, B·S not a multiple of S-tiles
+    (1, 125, 16, 8, 8, 2048, True),    # short song: split-K partials + standalone head_post
 ])
 def test_gemm_headpost_vs_oracle(gpu_device, B, S, nq, nk, nv, K, rope):
     ff = _ff()
@@ -68,8 +69,10 @@ def test_gemm_headpost_vs_oracle(gpu_device, B, S, nq, nk, nv, K, rope):
         ff.ptr(v) if nv else None, ff.stream_ptr()), "gemm_headpost")
     # same GEMM tile (variant 8) with the plain store epilogue → identical bf16(acc)
     C = torch.empty(B * S, N, dtype=torch.bfloat16, device=gpu_device)
-    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(Ad), K, ff.ptr(Wd), K, ff.ptr(C), N, B * S, N, K, None, 0, 8,
-                                          ff.stream_ptr()), "gemm")
+    # (short songs take the split-K path: its plain-store twin is the production dispatch, -1)
+    split = ((B * S + 127) // 128) * (N // 128) * 2 <= 256 and K // 64 >= 8
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(Ad), K, ff.ptr(Wd), K, ff.ptr(C), N, B * S, N, K, None, 0,
+                                          -1 if split else 8, ff.stream_ptr()), "gemm")
     torch.cuda.synchronize()
     rq, rk, rv = _headpost_ref(C.cpu(), B, S, nq, nk, nv, qw, kw, cos, sin, 1e-6)
     for got, ref in ((q, rq), (k, rk), (v, rv)):
