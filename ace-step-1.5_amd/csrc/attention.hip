@@ -393,6 +393,13 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.nsplit = min(4, cus / tail);
         sp.cnt = (int *)ws;
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
+    } else if (ws && nrep == 2 && window < 0 && units * 2 <= cus && unit_tiles >= 4) {
+        // short sequences (a few query blocks): every unit split over KV ranges so the
+        // grid reaches the CUs (cross-attention of a 10 s song: 8 units → 40 parts)
+        sp.full = 0;
+        sp.nsplit = min(min(cus / units, unit_tiles / 2), 16);
+        sp.cnt = (int *)ws;
+        sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
     }
     const int grid = sp.full + (units - sp.full) * sp.nsplit;
     if (nrep == 2) {

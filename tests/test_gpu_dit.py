@@ -113,7 +113,9 @@ def _attn_ref(q, k, v, window):
                                                   (1, 2, 1, 50, 20, -1), (1, 2, 1, 3000, 3000, 128),
                                                   # DiT shapes at 240 s: 384 units on 256 CUs → tail split
                                                   (2, 16, 8, 3000, 3000, -1), (2, 16, 8, 3000, 3000, 128),
-                                                  (2, 16, 8, 3000, 641, -1)])
+                                                  (2, 16, 8, 3000, 641, -1),
+                                                  # 10 s song: 8 units → every unit KV-split
+                                                  (1, 16, 8, 125, 641, -1), (1, 16, 8, 125, 125, 128)])
 def test_attention(gpu_device, B, H, KV, Sq, Sk, window):
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(Sq * 7 + Sk)
