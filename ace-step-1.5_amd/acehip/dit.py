@@ -128,6 +128,10 @@ class DiTRuntime:
                                        ptr(out), stream_ptr()), "dit_forward")
         return out
 
+    def use_graph(self, enable: bool = True):
+        """Replay the layer stack of every forward as one captured HIP graph (default off: measured neutral)."""
+        check(lib().acehip_dit_set_graph(self.h, 1 if enable else 0), "dit_set_graph")
+
     PROFILE_KINDS = ["gemm_swiglu", "gemm_down", "gemm_qkv", "gemm_o", "attn_full", "attn_band",
                      "attn_cross"]
 

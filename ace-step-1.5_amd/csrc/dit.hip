@@ -83,7 +83,17 @@ struct acehip_dit {
     std::vector<hipEvent_t> ev;        // 2·NPAIR events
     std::vector<int> ev_kind;          // kind of each recorded pair
     int ev_used = 0;
+
+    // HIP graph of the forward's pointer-independent middle (acehip_dit_set_graph): the
+    // timestep MLPs, modulation, proj_in and the layer stack read and write only handle
+    // buffers, so one capture per (Bc, S, Lenc, uniform_from) replays for every step
+    bool graph_on = false;
+    hipStream_t cap_stream = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    int gkey[4] = {-1, -1, -1, -1};
 };
+
+static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s);
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
 static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
@@ -187,6 +197,8 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->sliding.resize(h->L);
     for (int i = 0; i < h->L; ++i) h->sliding[i] = cfg->sliding ? cfg->sliding[i] : ((i + 1) % 2);
     h->cfg.sliding = nullptr;
+    const char *ge = getenv("ACEHIP_DIT_GRAPH");
+    h->graph_on = ge && ge[0] == '1';
     const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L;
     bool ok = true;
     auto A = [&](size_t n) { bf16_t *p = dalloc(h, n); ok = ok && p; return p; };
@@ -404,6 +416,7 @@ int acehip_dit_set_weight(acehip_dit *h, const char *name, const void *ptr, int 
 int acehip_dit_finalize(acehip_dit *h) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
     HIP_TRY(hipSetDevice(h->device));
+    if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }   // re-capture
     std::string missing;
     for (auto &kv : h->slots)
         if (!kv.second.set) missing += kv.first + " ";
@@ -483,6 +496,54 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     if (T <= 0 || S > h->cfg.max_S || Bx <= 0 || Bc % Bx) return fail(ACEHIP_E_ARG, "forward: T/Bx out of range");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    const int M = Bc * S;
+    int rc;
+#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
+    // the only reads of t / xt / ctx: sinusoid embeddings and patch packing (base:1340-1358)
+    for (int e = 0; e < 2; ++e) RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
+    RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
+    if (!h->graph_on || h->prof) {
+        RUN(forward_body(h, Bc, S, s));
+    } else {
+        const int key[4] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc)};
+        if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
+            if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
+            if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+            HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
+            const int brc = forward_body(h, Bc, S, h->cap_stream);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
+            if (brc) { if (g) (void)hipGraphDestroy(g); return brc; }
+            if (ec != hipSuccess || !g) return fail(ACEHIP_E_HIP, "forward: graph capture failed");
+            const hipError_t ei = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ei != hipSuccess) { h->gexec = nullptr; return fail(ACEHIP_E_HIP, "forward: graph instantiate failed"); }
+            memcpy(h->gkey, key, sizeof(key));
+        }
+        HIP_TRY(hipGraphLaunch(h->gexec, s));
+    }
+    // proj_out (base:1491-1501) on the normed output XN
+    GemmArgs po{};
+    po.A = h->XN; po.lda = h->D; po.W = h->wout; po.ldw = h->D;
+    po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
+    po.M = M; po.N = 128; po.K = h->D; po.epi = EPI_STORE; po.bias = h->bout;
+    RUN(hgemm(h, po, s));
+    if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
+#undef RUN
+    return 0;
+}
+
+int acehip_dit_set_graph(acehip_dit *h, int enable) {
+    if (!h) return fail(ACEHIP_E_ARG, "null handle");
+    h->graph_on = enable != 0;
+    return 0;
+}
+
+}  // extern "C"
+
+// Everything of one forward between the input packing and proj_out: reads only handle
+// buffers (emb, Xin, weights, K/V cache), so it can be captured once and replayed.
+static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s) {
     const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L, M = Bc * S;
     const int H = h->cfg.heads, KV = h->cfg.kv_heads, Le = h->cond_Lenc;
     const float eps = h->cfg.eps, scale = 1.0f / sqrtf((float)h->cfg.head_dim);
@@ -490,7 +551,6 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
 #define RUN(x) do { if ((rc = (x))) return rc; } while (0)
     // timestep embeddings: temb = temb_t + temb_r, proj = proj_t + proj_r (base:1340-1344)
     for (int e = 0; e < 2; ++e) {
-        RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
         RUN(gemv_small(h->emb[e], 256, h->te_l1[e], h->te_b1[e], h->h1, D, Bc, D, 256, 0, s));
         RUN(gemv_small(h->h1, D, h->te_l2[e], h->te_b2[e], h->temb_e[e], D, Bc, D, D, 1, s));
         RUN(gemv_small(h->temb_e[e], D, h->te_tp[e], h->te_btp[e], h->proj_e[e], 6 * D, Bc, 6 * D, D, 1, s));
@@ -500,8 +560,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s));
     RUN(modulation(h->sst_out, 1, 2, h->temb, Bc, D, h->mod_out, s));
 
-    // proj_in (base:1347-1358)
-    RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
+    // proj_in (base:1347-1358) over the packed patches Xin
     GemmArgs g{};
     g.A = h->Xin; g.lda = 384; g.W = h->win; g.ldw = 384; g.C = h->X; g.ldc = D;
     g.M = M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
@@ -562,17 +621,13 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
         RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s); }));
     }
-    // norm_out AdaLN + proj_out (base:1491-1501)
+    // norm_out AdaLN (base:1491-1497); proj_out runs after the body
     RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s));
-    GemmArgs po{};
-    po.A = h->XN; po.lda = D; po.W = h->wout; po.ldw = D;
-    po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
-    po.M = M; po.N = 128; po.K = D; po.epi = EPI_STORE; po.bias = h->bout;
-    RUN(hgemm(h, po, s));
-    if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
 #undef RUN
     return 0;
 }
+
+extern "C" {
 
 int acehip_dit_profile(acehip_dit *h, int enable) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
@@ -615,6 +670,8 @@ int acehip_dit_destroy(acehip_dit *h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);
     for (auto &e : h->ev) (void)hipEventDestroy(e);
+    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     for (void *p : h->allocs) (void)hipFree(p);
     delete h;
     return 0;

@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--lenc", type=int, default=641)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-vae", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each forward's layer stack as a captured HIP graph (measured neutral; off by default)")
     p.add_argument("--no-condition", action="store_true",
                    help="feed synthetic encoder states directly (skip the HIP condition encoders)")
     p.add_argument("--lyric-len", type=int, default=512)
@@ -125,6 +127,7 @@ def main():
     null = synth_null_condition(cfg, seed=0, device=dev, dtype=torch.bfloat16, backend="torch")
     rt = DiTRuntime(cfg, local, max_S=S, max_Bc=Bc, max_Lenc=args.lenc)
     rt.load(W)
+    rt.use_graph(args.graph)
     prep = None
     if not args.no_condition:
         # lyric + timbre + text encoders on the HIP path; Lenc = lyric + 1 timbre + text

@@ -112,6 +112,15 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx,
                        const float *t, const float *t_r, int t_stride, int Bc, int T,
                        void *vt_out, void *stream);
 
+/* Replay the pointer-independent middle of acehip_dit_forward (timestep MLPs,
+ * modulation, proj_in, the layer stack, norm_out) as one HIP graph, captured
+ * once per (Bc, S, Lenc, uniform rows) and re-captured when they change or
+ * after finalize.  Default off (ACEHIP_DIT_GRAPH=1 turns it on at create):
+ * measured neutral on MI355X (0.600 vs 0.602 s/song, turbo 10 s 38.8 vs
+ * 39.2 ms) — kernel-to-kernel gaps are not launch-bound here.  Profiling runs
+ * the eager path.  Results are bit-identical either way. */
+int acehip_dit_set_graph(acehip_dit *h, int enable);
+
 int acehip_dit_destroy(acehip_dit *h);
 
 /* Per-kernel HIP-event timing inside acehip_dit_forward (for the bench's

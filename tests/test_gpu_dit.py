@@ -428,3 +428,37 @@ def test_gemm_splitk_small_m(gpu_device, M, N, K):
     y = ref.bfloat16().float().view(M, N // 64, 2, 32)
     gate, up = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
     assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2
+
+
+def test_forward_graph_replay_matches_eager(gpu_device):
+    """acehip_dit_set_graph: the captured layer-stack graph gives bit-identical outputs to
+    eager launches across new t / xt / out pointers, a new condition of the same shape,
+    a sequence-length change (re-capture) and the CFG uniform-row toggle."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=4, window=8)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=4, mode="parity").items()}
+    g = torch.Generator().manual_seed(11)
+    rt = DiTRuntime(cfg, 0, max_S=64, max_Bc=4, max_Lenc=40)
+    rt.load(W)
+
+    def both(xt, ctx, t):
+        rt.use_graph(False)
+        a = rt.forward(xt, ctx, t).clone()
+        rt.use_graph(True)
+        b = rt.forward(xt, ctx, t)
+        c = rt.forward(xt, ctx, t)          # replay of the same capture
+        torch.cuda.synchronize()
+        assert torch.equal(a, b) and torch.equal(a, c)
+        return a
+
+    for T, Le, seed_t in [(100, 37, 0.625), (100, 37, 0.25), (77, 37, 0.5), (100, 21, 0.9)]:
+        xt = torch.randn(2, T, 64, generator=g).bfloat16().to(gpu_device)
+        ctx = torch.randn(2, T, 128, generator=g).bfloat16().to(gpu_device)
+        enc = torch.randn(2, Le, cfg.hidden_size, generator=g).bfloat16()
+        null = torch.randn(1, 1, cfg.hidden_size, generator=g).bfloat16()
+        rt.set_condition(torch.cat([enc, null.expand_as(enc)]).to(gpu_device))
+        t = torch.tensor([seed_t], dtype=torch.float32, device=gpu_device)
+        both(xt, ctx, t)
+        rt.set_uniform_rows(2)
+        both(xt, ctx, t)
+    rt.close()
