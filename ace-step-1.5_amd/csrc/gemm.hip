@@ -687,6 +687,37 @@ static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
     return 0;
 }
 
+// Tail split for ping-pong grids whose last round is a small fraction of the chip
+// (SwiGLU gate/up at 240 s: 24 × 48 = 1152 tiles of 256² on 256 CUs = 4.5 rounds, the
+// last half-round costing a whole tile time): rows [0, M1) keep the big tile with
+// M1 chosen so their grid is whole rounds (less at most one row of tiles), and the
+// remaining rows run as one round of 128×128 tiles (2 blocks/CU).  Row-local
+// epilogues only (store / SwiGLU; the gated residual indexes its batch by row).
+// ACEHIP_GEMM_TAILSPLIT=0 disables it, =<digit> picks the tail variant (A/B).  Returns 1 when not applicable.
+static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
+    if (a.epi != EPI_SWIGLU && a.epi != EPI_STORE) return 1;
+    const char *e = getenv("ACEHIP_GEMM_TAILSPLIT");
+    if (e && e[0] == '0') return 1;
+    const int BMv = v == 7 ? 256 : 192, cus = num_cus();
+    const int64_t nN = a.N / 256, tiles = (int64_t)((a.M + BMv - 1) / BMv) * nN;
+    const int64_t full = tiles / cus, rem = tiles - full * cus;
+    if (full < 1 || rem == 0 || rem * 5 > (int64_t)cus * 3) return 1;   // last round > 60 % full
+    const int64_t M1 = (full * cus / nN) * BMv;
+    if (M1 <= 0 || M1 >= a.M) return 1;
+    const int tv = (e && e[0] >= '2' && e[0] <= '9') ? e[0] - '0' : 0;   // tail variant (A/B)
+    const int64_t tail_bn = (tv == 3 || tv == 5 || tv == 6) ? 256 : 128;
+    if (((a.M - M1 + 127) / 128) * (a.N / tail_bn) > 2 * (int64_t)cus) return 1;
+    GemmArgs hd = a;
+    hd.M = (int)M1;
+    int rc = gemm_variant(hd, v, s);
+    if (rc) return rc;
+    GemmArgs tl = a;
+    tl.M = a.M - (int)M1;
+    tl.A = a.A + M1 * a.lda;
+    tl.C = a.C + M1 * a.ldc;
+    return gemm_variant(tl, tv, s);
+}
+
 int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.M <= 0) return 0;
     if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
@@ -713,7 +744,13 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         return launch_pp<192>(a, s);   // the fused epilogue exists for the 192-row tile only
     }
     int v = g_variant_override;
-    if (v < 0) v = gemm_pick_variant(a.M, a.N);
+    if (v < 0) {
+        v = gemm_pick_variant(a.M, a.N);
+        if (v == 7 || v == 8) {
+            const int rc = gemm_tail_split(a, v, s);
+            if (rc <= 0) return rc;   // split done (0) or failed (< 0); 1 = not applicable
+        }
+    }
     if ((v == 3 || v >= 5) && a.N % 256) v = 0;
     return gemm_variant(a, v, s);
 }

@@ -462,3 +462,36 @@ def test_forward_graph_replay_matches_eager(gpu_device):
         rt.set_uniform_rows(2)
         both(xt, ctx, t)
     rt.close()
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(6000, 12288, 2048, EPI_SWIGLU), (15000, 12288, 2048, EPI_SWIGLU),
+                                       (6000, 12288, 2048, EPI_STORE)])
+def test_gemm_tail_split(gpu_device, monkeypatch, M, N, K, epi):
+    """Ping-pong grids with a small last round run their tail rows as one round of 128x128
+    tiles (gemm_tail_split): vs fp32 torch, and vs the unsplit launch."""
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(gpu_device, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    ncol = N // 2 if epi == EPI_SWIGLU else N
+
+    def run(split):
+        monkeypatch.setenv("ACEHIP_GEMM_TAILSPLIT", "1" if split else "0")
+        C = torch.full((M, ncol), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), ncol, M, N, K, None, epi, -1,
+                                              ff.stream_ptr()))
+        torch.cuda.synchronize()
+        return C.float()
+
+    on, off = run(True), run(False)
+    assert torch.isfinite(on).all()
+    if epi == EPI_SWIGLU:
+        y = ref.bfloat16().float().view(M, N // 64, 2, 32)
+        gate, up = y[:, :, 0, :].reshape(M, ncol), y[:, :, 1, :].reshape(M, ncol)
+        want = torch.nn.functional.silu(gate).bfloat16().float() * up
+        tol = 1e-2
+    else:
+        want, tol = ref, 5e-3
+    assert rel_l2(on.cpu(), want.cpu()) < tol
+    assert rel_l2(on.cpu(), off.cpu()) < tol
