@@ -741,7 +741,25 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         if (a.N % 256 || h.S <= 0 || (int64_t)h.B * h.S != a.M || (h.nq + h.nk + h.nv) * 128 != a.N ||
             h.S_dst < h.S || (h.nq && !h.qw) || (h.nk && !h.kw) || (h.cos == nullptr) != (h.sin == nullptr))
             return fail(-1, "gemm: head-post arguments inconsistent with the GEMM shape");
-        return launch_pp<192>(a, s);   // the fused epilogue exists for the 192-row tile only
+        // the fused epilogue exists for the 192-row tile only; a grid of it that fills at
+        // most half the chip (cross-Q of the conditional rows, M = 3000) runs as 128×128
+        // tiles into the staging buffer + the standalone head_post kernel instead
+        const int64_t t192 = (int64_t)((a.M + 191) / 192) * (a.N / 256);
+        const char *e = getenv("ACEHIP_GEMM_HP128");
+        if (a.ws && t192 * 2 <= num_cus() && (size_t)a.M * a.N * 2 <= a.ws_bytes && !(e && e[0] == '0')) {
+            GemmArgs st = a;
+            st.epi = EPI_STORE;
+            st.bias = nullptr;
+            st.C = (bf16_t *)a.ws;
+            st.ldc = a.N;
+            int rc = gemm_variant(st, 0, s);
+            if (rc) return rc;
+            HeadPostArgs hh = a.hp;
+            hh.src = st.C;
+            hh.ld_src = a.N;
+            return head_post(hh, s);
+        }
+        return launch_pp<192>(a, s);
     }
     int v = g_variant_override;
     if (v < 0) {
