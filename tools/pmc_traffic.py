@@ -53,7 +53,18 @@ if __name__ == "__main__":
         doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace on tools/prof_dit.py "
                          "(separate passes; FETCH x2 gfx950 correction; KB -> bytes)",
                "kernels": t}
-        if sw:
+        M = int(sys.argv[4]) if len(sys.argv) > 4 else 6000   # Bc·S of the profiled run
+        # one SwiGLU GEMM call = the 256² ping-pong grid over rows [0, M1) + the tail rows as
+        # 128×128 tiles (gemm_tail_split, gemm.hip; 256 CUs, N = 12288 → 48 column tiles)
+        M1 = (((M + 255) // 256 * 48) // 256 * 256 // 48) * 256
+        keys = [f"gemm_pp_kernel<256, 3> grid={(M1 // 256) * 48 * 512}"]
+        if M1 < M:
+            keys.append(f"gemm_kernel<128, 128, 2, 2, 2, 3> grid={((M - M1 + 127) // 128) * 96 * 256}")
+        if all(k in t for k in keys):
+            doc["gemm_swiglu_hbm_bytes_per_launch"] = sum(t[k]["hbm_bytes"] for k in keys)
+            doc["gemm_swiglu_kernels"] = keys
+            doc["gemm_swiglu_M"] = M
+        elif sw:
             doc["gemm_swiglu_hbm_bytes_per_launch"] = max(v["hbm_bytes"] for v in sw)
-            doc["gemm_swiglu_M"] = int(sys.argv[4]) if len(sys.argv) > 4 else 6000   # Bc·S of the profiled run
+            doc["gemm_swiglu_M"] = M
         json.dump(doc, open(sys.argv[3], "w"), indent=1)
