@@ -19,7 +19,10 @@ from acehip import _ffi as ff  # noqa: E402
 
 dev = torch.device("cuda:0")
 S = int(os.environ.get("ATTN_S", "3000"))
-SHAPES = {"full": (2, 16, 8, S, S, -1), "band": (2, 16, 8, S, S, 128), "cross": (2, 16, 8, S, 641, -1)}
+SHAPES = {"full": (2, 16, 8, S, S, -1), "band": (2, 16, 8, S, S, 128), "cross": (2, 16, 8, S, 641, -1),
+          "cross1": (1, 16, 8, S, 641, -1)}
+if os.environ.get("SHAPES"):
+    SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 
 
 def flops(B, H, Sq, Sk, w):
