@@ -38,13 +38,15 @@ class EncoderStack:
     norm (→ proj_out), reference base:374-440."""
 
     def __init__(self, cfg: DiTConfig, n_layers: int, in_dim: int, embed_bias: bool = True,
-                 out_dim: int = 0, device: int = 0, max_tokens: int = 8192, max_S: int = 4096):
+                 out_dim: int = 0, device: int = 0, max_tokens: int = 8192, max_S: int = 4096,
+                 causal: bool = False):
         self.cfg = cfg
         self.device = torch.device("cuda", device)
         self.D = cfg.hidden_size
         self.out_dim = out_dim
         self.max_tokens, self.max_S = max_tokens, max_S
-        sl = (_ffi.c_uint8 * max(n_layers, 1))(*[1 if cfg.is_sliding(i) else 0 for i in range(n_layers)])
+        kinds = [2 if causal else (1 if cfg.is_sliding(i) else 0) for i in range(n_layers)]
+        sl = (_ffi.c_uint8 * max(n_layers, 1))(*kinds)
         self._sliding = sl
         c = _ffi.EncCfg(hidden=cfg.hidden_size, intermediate=cfg.intermediate_size,
                         heads=cfg.num_attention_heads, kv_heads=cfg.num_key_value_heads,
@@ -111,6 +113,77 @@ class EncoderStack:
             self.close()
         except Exception:
             pass
+
+
+class _EmbedTokens:
+    """``text_encoder.embed_tokens(ids)``: the embedding-table row gather (index plumbing
+    on the device, as the reference's nn.Embedding does it)."""
+
+    def __init__(self, table: torch.Tensor):
+        self.weight = table
+
+    def __call__(self, input_ids: torch.Tensor) -> torch.Tensor:
+        return torch.nn.functional.embedding(input_ids.to(self.weight.device), self.weight)
+
+
+class TextEncoderOutput:
+    def __init__(self, last_hidden_state: torch.Tensor):
+        self.last_hidden_state = last_hidden_state
+
+
+class TextEncoder:
+    """Qwen3-Embedding-0.6B (``Qwen3Model``) drop-in for the reference's ``text_encoder``
+    (loaded at ``init_service_loader.py:146-160``, called by ``infer_text_embeddings`` /
+    ``infer_lyric_embeddings``, ``conditioning_embed.py:71-79``):
+    ``text_encoder(input_ids=ids, lyric_attention_mask=None).last_hidden_state`` and
+    ``text_encoder.embed_tokens(ids)``.  The 28 causal Qwen3 decoder layers and the final
+    norm run on the ``acehip_enc`` runtime (every layer causal, no embed Linear); the
+    embedding lookup is a device gather.  Like the reference call (no ``attention_mask``)
+    the mask is Qwen3Model's default causal one; a padding mask is not supported."""
+
+    QWEN3_06B = dict(hidden_size=1024, intermediate_size=3072, num_hidden_layers=28, num_attention_heads=16,
+                     num_key_value_heads=8, head_dim=128, rms_norm_eps=1e-6, rope_theta=1_000_000.0)
+
+    def __init__(self, cfg: Optional[DiTConfig] = None, device: int = 0, max_batch: int = 8, max_tokens: int = 512):
+        self.cfg = cfg or DiTConfig(**self.QWEN3_06B)
+        self.device = torch.device("cuda", device)
+        self.stack = EncoderStack(self.cfg, self.cfg.num_hidden_layers, 0, device=device,
+                                  max_tokens=max_batch * max_tokens, max_S=max_tokens, causal=True)
+        self.embed_tokens: Optional[_EmbedTokens] = None
+
+    @classmethod
+    def from_reference_model(cls, model, **kw) -> "TextEncoder":
+        """From the reference's loaded ``AutoModel`` (a transformers ``Qwen3Model``)."""
+        c = model.config
+        cfg = DiTConfig(hidden_size=c.hidden_size, intermediate_size=c.intermediate_size,
+                        num_hidden_layers=c.num_hidden_layers, num_attention_heads=c.num_attention_heads,
+                        num_key_value_heads=c.num_key_value_heads,
+                        head_dim=getattr(c, "head_dim", c.hidden_size // c.num_attention_heads),
+                        rms_norm_eps=c.rms_norm_eps, rope_theta=_rope_theta(c))
+        te = cls(cfg, **kw)
+        te.load(model.state_dict())
+        return te
+
+    def load(self, weights: Dict[str, torch.Tensor]):
+        """Qwen3Model state-dict names (``embed_tokens.weight``, ``layers.N.…``, ``norm.weight``)."""
+        w = {k: v for k, v in weights.items() if k != "embed_tokens.weight"}
+        self.embed_tokens = _EmbedTokens(weights["embed_tokens.weight"].detach().to(self.device, torch.bfloat16))
+        self.stack.load(w)
+
+    def __call__(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                 **kwargs) -> TextEncoderOutput:
+        if attention_mask is not None:
+            raise NotImplementedError("TextEncoder: padding masks are not supported (the reference passes none)")
+        h = self.embed_tokens(input_ids)
+        return TextEncoderOutput(self.stack.forward(h))
+
+    def close(self):
+        self.stack.close()
+
+
+def _rope_theta(c) -> float:
+    rp = getattr(c, "rope_parameters", None) or {}
+    return float(rp.get("rope_theta", getattr(c, "rope_theta", 1_000_000.0)))
 
 
 def unpack_timbre(emb: torch.Tensor, order: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

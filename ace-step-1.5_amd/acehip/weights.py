@@ -125,6 +125,20 @@ def tokenizer_weight_shapes(cfg: DiTConfig) -> Dict[str, Shape]:
     return s
 
 
+def text_encoder_shapes(cfg: DiTConfig, vocab: int) -> Dict[str, Shape]:
+    """Qwen3Model (the Qwen3-Embedding-0.6B text encoder) state-dict names: embed_tokens
+    (an nn.Embedding table), the decoder layers, the final norm."""
+    s: Dict[str, Shape] = {"embed_tokens.weight": (vocab, cfg.hidden_size)}
+    for k, v in encoder_stack_shapes(cfg, "_", cfg.num_hidden_layers, 0, False).items():
+        if not k.startswith("_.embed_tokens"):
+            s[k[2:]] = v
+    return s
+
+
+def synth_text_encoder_weights(cfg: DiTConfig, vocab: int, seed: int = 0, mode: str = "bench", **kw):
+    return synth_weights(text_encoder_shapes(cfg, vocab), seed, mode, **kw)
+
+
 def synth_tokenizer_weights(cfg: DiTConfig, seed: int = 0, mode: str = "bench", **kw):
     return synth_weights(tokenizer_weight_shapes(cfg), seed, mode, **kw)
 

@@ -124,10 +124,12 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
     int kv_lo = 0, kv_hi = Sk;
     const uint8_t *km = kmask ? kmask + (int64_t)b * Sk : nullptr;
+    const bool causal = window == ATTN_CAUSAL;   // kernel-uniform: keys j <= i only
     if (window >= 0 && !km) {
         kv_lo = max(0, qblk - window);
         kv_hi = min(Sk, qblk + QB + window);
     }
+    if (causal) kv_hi = min(Sk, qblk + QB);
     const int wlim = window >= 0 ? window : 0x7fffffff;
     int t_first = kv_lo / KT;
     int ntiles = (kv_hi + KT - 1) / KT - t_first;
@@ -202,9 +204,11 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         if (defer && it > 0) pv(lds + ((it + NBUF - 1) % NBUF) * 2 * TILE + TILE, pf);
         // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
         // skipped (the wave still joins the barrier); one entirely inside needs no mask
-        const bool outside = window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window);
+        const bool outside = (window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window)) ||
+                             (causal && kv0 > q0 + 31);
         const bool interior = !km && kv0 + KT <= Sk &&
-                              (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window));
+                              (causal ? kv0 + KT - 1 <= q0
+                                      : (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window)));
         if (outside && !defer) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                     const int kj = kv0 + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
                     // branch-free: window < 0 ⇒ wlim = INT_MAX
                     const bool inr = kj < Sk;
-                    bool ok = inr & (abs(qi - kj) <= wlim);
+                    bool ok = inr & (abs(qi - kj) <= wlim) & (!causal | (kj <= qi));
                     float bad = NEG;
                     if (km) {   // key-padding mode (uniform over branches: km is kernel-uniform)
                         ok = ok && km[inr ? kj : 0] != 0;
@@ -388,7 +392,10 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // only long KV loops pay for the partial write + merge (measured: full attention
     // at S = 3000, 47 tiles, −27 %; band (≈7 tiles) and cross (11 tiles) lose)
     const int unit_tiles = (window >= 0 && !kmask) ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
-    if (ws && nrep == 2 && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
+    if (window == ATTN_CAUSAL) {
+        // causal (text encoder): whole units only — a KV-range part past the diagonal
+        // would hold no valid key
+    } else if (ws && nrep == 2 && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
         sp.full = units - tail;
         sp.nsplit = min(4, cus / tail);
         sp.cnt = (int *)ws;

@@ -7,7 +7,9 @@
 // 8 layers, key-padding mask), the timbre encoder (base:997-1178, 4 layers,
 // no mask), the attention pooler (base:734-859) and the detokenizer
 // (base:862-994); the host composes them into AceStepConditionEncoder
-// (base:1509-1554).  The layer reuses the DiT's kernels unchanged:
+// (base:1509-1554).  With every layer causal (sliding[l] == 2) and no embed
+// Linear it is also the Qwen3-Embedding-0.6B text encoder (Qwen3Model, the
+// reference's infer_text_embeddings, conditioning_embed.py:71-74).  The layer reuses the DiT's kernels unchanged:
 //
 //   XN = RMSNorm(X)                              rmsnorm_mod (plain)
 //   q|k|v = XN·Wqkvᵀ → q/k RMSNorm + RoPE → head-major     gemm EPI_HEADPOST
@@ -277,8 +279,9 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
         RUN(hgemm(h, q, s));
-        RUN(attention(h->Qh, h->Kh, h->Vh, h->AO, B, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1, scale, qd,
-                      h->attn_ws, s, kmask));
+        // layer kind: 0 full, 1 band |i−j| <= window, 2 causal (the Qwen3 text encoder)
+        const int win = h->sliding[l] == 2 ? ATTN_CAUSAL : h->sliding[l] ? h->cfg.window : -1;
+        RUN(attention(h->Qh, h->Kh, h->Vh, h->AO, B, H, KV, S, S, win, scale, qd, h->attn_ws, s, kmask));
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_RES; o.res = h->X; o.ldr = D;

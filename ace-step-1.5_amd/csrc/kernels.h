@@ -85,6 +85,8 @@ int head_post(const HeadPostArgs &a, hipStream_t s);
 // ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials
 // + self-resetting counters), or null to disable tail balancing.
 // kmask: optional key-padding mask [B][Sk] (1 = attend), encoder semantics (attention.hip header)
+// window: < 0 full, >= 0 band |i−j| <= window, ATTN_CAUSAL keys j <= i (Qwen3 text encoder)
+constexpr int ATTN_CAUSAL = -2;
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
               int Sq, int Sk, int window, float scale, int64_t o_ld, void *ws, hipStream_t s,
               const uint8_t *kmask = nullptr);

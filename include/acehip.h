@@ -158,7 +158,8 @@ typedef struct acehip_enc_cfg {
     float rope_theta;    /* 1e6 */
     int max_tokens;      /* max B*S per forward */
     int max_S;           /* max sequence length */
-    const uint8_t *sliding; /* [layers] 1 = sliding layer; NULL = even idx */
+    const uint8_t *sliding; /* [layers] 1 = sliding layer, 2 = causal (Qwen3
+                             * text encoder, Qwen3Model's default mask); NULL = even idx */
 } acehip_enc_cfg;
 
 typedef struct acehip_enc acehip_enc;
@@ -287,7 +288,8 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 
 /* Flash attention, head_dim 128, GQA: q [B,H,Sq,128], k/v [B,KV,Sk,128] →
- * o [B,Sq,H*128]; window < 0 = full, else |i-j| <= window. */
+ * o [B,Sq,H*128]; window -1 = full, >= 0 |i-j| <= window, -2 = causal
+ * (keys j <= i; the Qwen3 text encoder's default mask). */
 int acehip_attention_bf16(const void *q, const void *k, const void *v, void *o, int B, int H,
                           int KV, int Sq, int Sk, int window, float scale, void *stream);
 /* Same with a key-padding mask kmask uint8 [B, Sk] (1 = attend), encoder semantics. */

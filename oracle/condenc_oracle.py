@@ -210,3 +210,20 @@ def audio_tokenizer(W, cfg, x: Tensor) -> Tuple[Tensor, Tensor]:
     h = F.linear(x, W["tokenizer.audio_acoustic_proj.weight"], W["tokenizer.audio_acoustic_proj.bias"])
     h = attention_pooler(W, cfg, h)
     return residual_fsq(W, h)
+
+
+def text_encoder(W: Dict[str, Tensor], cfg, input_ids: Tensor) -> Tensor:
+    """Qwen3Model.forward as the reference calls it (``conditioning_embed.py:71-74``: no
+    attention mask ⇒ the default causal mask): embedding lookup, Qwen3 decoder layers
+    (same structure as AceStepEncoderLayer) under a causal additive mask, final norm.
+    Weights: Qwen3Model state-dict names."""
+    h = F.embedding(input_ids, W["embed_tokens.weight"])
+    S, dt = h.shape[1], h.dtype
+    idx = torch.arange(S)
+    mask = torch.full((1, 1, S, S), torch.finfo(dt).min, dtype=dt).masked_fill_(
+        (idx[None, :] <= idx[:, None])[None, None], 0.0)
+    cos, sin = rope_tables(S, cfg.head_dim, cfg.rope_theta, dt)
+    cos, sin = cos.unsqueeze(1), sin.unsqueeze(1)
+    for i in range(cfg.num_hidden_layers):
+        h = encoder_layer(W, f"layers.{i}", cfg, h, mask, cos, sin)
+    return rms_norm(h, W["norm.weight"], cfg.rms_norm_eps)

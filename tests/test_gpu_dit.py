@@ -101,10 +101,12 @@ def _attn_ref(q, k, v, window):
     k = k.float().repeat_interleave(rep, 1)
     v = v.float().repeat_interleave(rep, 1)
     s = (q.float() @ k.transpose(2, 3)) / math.sqrt(128)
+    i = torch.arange(Sq, device=q.device)[:, None]
+    j = torch.arange(Sk, device=q.device)[None, :]
     if window >= 0:
-        i = torch.arange(Sq, device=q.device)[:, None]
-        j = torch.arange(Sk, device=q.device)[None, :]
         s = s.masked_fill((i - j).abs() > window, float("-inf"))
+    elif window == -2:                                  # causal (Qwen3 text encoder)
+        s = s.masked_fill(j > i, float("-inf"))
     return torch.softmax(s, -1) @ v
 
 
@@ -115,7 +117,10 @@ def _attn_ref(q, k, v, window):
                                                   (2, 16, 8, 3000, 3000, -1), (2, 16, 8, 3000, 3000, 128),
                                                   (2, 16, 8, 3000, 641, -1),
                                                   # 10 s song: 8 units → every unit KV-split
-                                                  (1, 16, 8, 125, 641, -1), (1, 16, 8, 125, 125, 128)])
+                                                  (1, 16, 8, 125, 641, -1), (1, 16, 8, 125, 125, 128),
+                                                  # causal: text encoder (128 tokens), ragged, nrep 1
+                                                  (2, 16, 8, 128, 128, -2), (1, 16, 8, 77, 77, -2),
+                                                  (3, 4, 2, 300, 300, -2), (1, 2, 2, 257, 257, -2)])
 def test_attention(gpu_device, B, H, KV, Sq, Sk, window):
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(Sq * 7 + Sk)
