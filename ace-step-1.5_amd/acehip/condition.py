@@ -177,6 +177,13 @@ class TextEncoder:
         h = self.embed_tokens(input_ids)
         return TextEncoderOutput(self.stack.forward(h))
 
+    def to(self, *a, **k) -> "TextEncoder":
+        """The handler's offload context moves models with ``.to``; the handle stays resident."""
+        return self
+
+    def eval(self) -> "TextEncoder":
+        return self
+
     def close(self):
         self.stack.close()
 

@@ -37,7 +37,7 @@ from typing import Optional
 
 import torch
 
-from .condition import AudioDetokenizer, AudioTokenizer, ConditionEncoder, HipPrepareCondition
+from .condition import AudioDetokenizer, AudioTokenizer, ConditionEncoder, HipPrepareCondition, TextEncoder
 from .config import VAEConfig
 from .dit import AceStepDiTBackend
 from .vae import OobleckBackend
@@ -109,8 +109,8 @@ _LORA_METHODS = ("add_lora", "load_lora", "add_voice_lora", "remove_lora", "unlo
 
 
 def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: bool = False,
-            vae: bool = True, condition: bool = True) -> dict:
-    """Swap the handler's DiT sampler and VAE for the acehip backends."""
+            vae: bool = True, condition: bool = True, text_encoder: bool = True) -> dict:
+    """Swap the handler's DiT sampler, VAE and (Qwen3) text encoder for the acehip backends."""
     dit = AceStepDiTBackend.from_reference_model(handler.model, max_seconds=max_seconds,
                                                  max_batch=max_batch)
     if condition:
@@ -151,6 +151,12 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
             refresh_decoder_weights(dit, handler.model.decoder)
             return res
         setattr(handler, meth, wrapped)
+    if text_encoder and getattr(handler, "text_encoder", None) is not None:
+        # infer_text_embeddings / infer_lyric_embeddings (conditioning_embed.py:71-79)
+        te = TextEncoder.from_reference_model(handler.text_encoder, device=dit.rt.device.index or 0,
+                                              max_batch=max_batch)
+        handler.text_encoder = te
+        out["text_encoder"] = te
     if vae and getattr(handler, "vae", None) is not None:
         vb = vae_from_diffusers(handler.vae, max_seconds=max_seconds)
         orig_decode, orig_encode = handler.vae.decode, handler.vae.encode

@@ -98,14 +98,18 @@ def cpu_baseline(W_gpu, cfg, vae_w, vcfg, T, lenc):
     return {"dit_step_s": dit_s, "vae_window_s": vae_s, "threads": threads, "window": win}
 
 
+QWEN3_VOCAB = 151669   # Qwen3-Embedding-0.6B vocabulary
+
+
 def main():
     args = parse()
     from acehip import distributed as D
     from acehip.config import DiTConfig, VAEConfig
     from acehip.dit import AceStepDiTBackend, DiTRuntime
     from acehip.vae import OobleckBackend
-    from acehip.weights import synth_condenc_weights, synth_dit_weights, synth_null_condition, synth_vae_weights
-    from acehip.condition import ConditionEncoder, HipPrepareCondition
+    from acehip.weights import (synth_condenc_weights, synth_dit_weights, synth_null_condition,
+                                synth_text_encoder_weights, synth_vae_weights)
+    from acehip.condition import ConditionEncoder, HipPrepareCondition, TextEncoder
     from acehip.flops import dit_flops_per_row, vae_decoder_flops
 
     rank, world, local = D.env_world()
@@ -135,6 +139,12 @@ def main():
         ce.load(synth_condenc_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch"))
         prep = HipPrepareCondition(ce)
         args.lenc = args.lyric_len + 1 + args.text_len
+        # the Qwen3-Embedding-0.6B text encoder (infer_text_embeddings / infer_lyric_embeddings,
+        # conditioning_embed.py:71-79): 28 causal layers for the text tokens, the table for lyrics
+        te_cfg = DiTConfig(**TextEncoder.QWEN3_06B)
+        te = TextEncoder(te_cfg, local, max_batch=1, max_tokens=max(args.text_len, 64))
+        te.load(synth_text_encoder_weights(te_cfg, QWEN3_VOCAB, seed=0, mode="bench", device=dev,
+                                           dtype=torch.bfloat16, backend="torch"))
     be = AceStepDiTBackend(rt, null, is_turbo=args.turbo, prepare_condition=prep)
     vae = vae_w = None
     if not args.no_vae:
@@ -153,14 +163,13 @@ def main():
         D.broadcast_condition([enc, ctx])
         cond_kw = dict(encoder_hidden_states=enc, context_latents=ctx)
     else:
-        # text-encoder / lyric-embedding outputs and a 30 s timbre reference (the inputs of
-        # prepare_condition, base:1607-1652); the encoders run inside the timed song
-        text = torch.randn(1, args.text_len, cfg.text_hidden_dim, device=dev, generator=g).bfloat16()
-        lyric = torch.randn(1, args.lyric_len, cfg.text_hidden_dim, device=dev, generator=g).bfloat16()
+        # text / lyric token ids and a 30 s timbre reference; the text encoder and the
+        # condition encoders (prepare_condition, base:1607-1652) run inside the timed song
+        text_ids = torch.randint(0, QWEN3_VOCAB, (1, args.text_len), device=dev, generator=g)
+        lyric_ids = torch.randint(0, QWEN3_VOCAB, (1, args.lyric_len), device=dev, generator=g)
         refer = torch.randn(1, 750, cfg.timbre_hidden_dim, device=dev, generator=g).bfloat16()
-        D.broadcast_condition([text, lyric, refer, src])
-        cond_kw = dict(text_hidden_states=text, text_attention_mask=torch.ones(1, args.text_len, device=dev, dtype=torch.long),
-                       lyric_hidden_states=lyric,
+        D.broadcast_condition([text_ids, lyric_ids, refer, src])
+        cond_kw = dict(text_attention_mask=torch.ones(1, args.text_len, device=dev, dtype=torch.long),
                        lyric_attention_mask=torch.ones(1, args.lyric_len, device=dev, dtype=torch.long),
                        refer_audio_acoustic_hidden_states_packed=refer,
                        refer_audio_order_mask=torch.zeros(1, device=dev, dtype=torch.long),
@@ -191,6 +200,9 @@ def main():
         e1 = torch.cuda.Event(enable_timing=True)
         e2 = torch.cuda.Event(enable_timing=True)
         e0.record()
+        if not args.no_condition:
+            cond_kw.update(text_hidden_states=te(input_ids=text_ids, lyric_attention_mask=None).last_hidden_state,
+                           lyric_hidden_states=te.embed_tokens(lyric_ids))
         if span is not None:
             # vae.encode(x).latent_dist.sample() (vae_encode.py:65), then the repaint source:
             # encoded target with silence inside the span + chunk mask of the span
@@ -266,7 +278,7 @@ def main():
         "config": {"workload": f"text2music {args.seconds:g}s, "
                                + (f"turbo {args.infer_steps} steps (table, no CFG), " if args.turbo else
                                   f"base/sft {args.infer_steps} steps, shift {args.shift:g}, CFG {args.guidance:g} + APG, ")
-                               + ("DiT + VAE decode" if args.no_condition else "condition encoders + DiT + VAE decode")
+                               + ("DiT + VAE decode" if args.no_condition else "text encoder + condition encoders + DiT + VAE decode")
                                + (f", repaint [{args.repaint_start:g}, {args.repaint_end:g}) s: VAE encode first"
                                   if args.repaint else ""),
                    "global_batch": songs, "seq_len": S, "latent_frames": T, "lenc": args.lenc,
