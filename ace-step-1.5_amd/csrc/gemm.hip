@@ -660,13 +660,27 @@ int gemm_pick_variant(int64_t M, int N) {
 // reaches ~1 block per CU, every split stores fp32 partials, and one launch sums
 // them in order and applies the epilogue (the head-post case then runs the
 // standalone head_post kernel on the staged bf16 projection).
+// A/B knobs of the split-K path: ACEHIP_SPLITK_STAGES (2 | 3-stage LDS ring),
+// ACEHIP_SPLITK_FILL (target blocks per CU)
+// Default (tools/ab_splitk.py, M = 125): the 3-stage ring for N <= 4096 (down / QKV / O:
+// 20.1 → 19.0, 18.3 → 17.4, 15.1 → 14.9 µs), 2 stages for the wide SwiGLU (26.2 vs 28.3 µs)
+static int splitk_stages(int N) {
+    const char *e = getenv("ACEHIP_SPLITK_STAGES");
+    return e ? atoi(e) : (N <= 4096 ? 3 : 2);
+}
+static int splitk_fill() {
+    const char *e = getenv("ACEHIP_SPLITK_FILL");
+    return e ? std::max(1, atoi(e)) : 1;
+}
+
 static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
     GemmArgs p = a;
     const int nk = a.K / BK;
     p.kper = (nk + splits - 1) / splits;
     splits = (nk + p.kper - 1) / p.kper;
     const int tiles = ((a.M + 127) / 128) * (a.N / 128);
-    gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
+    if (splitk_stages(a.N) == 3) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
+    else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     HIP_TRY(hipGetLastError());
     bf16_t *out = a.C;
     int64_t ldo = a.ldc;
@@ -725,7 +739,8 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
         const int nk = a.K / BK;
         if (tiles * 2 <= cus && nk >= 8) {
-            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4), (cus + tiles - 1) / tiles);
+            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4),
+                                                (splitk_fill() * cus + tiles - 1) / tiles);
             const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
             if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s);
         }
