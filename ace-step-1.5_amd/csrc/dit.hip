@@ -90,10 +90,10 @@ struct acehip_dit {
     bool graph_on = false;
     hipStream_t cap_stream = nullptr;
     hipGraphExec_t gexec = nullptr;
-    int gkey[4] = {-1, -1, -1, -1};
+    int gkey[5] = {-1, -1, -1, -1, -1};
 };
 
-static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s);
+static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s);
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
 static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
@@ -502,15 +502,20 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     // the only reads of t / xt / ctx: sinusoid embeddings and patch packing (base:1340-1358)
     for (int e = 0; e < 2; ++e) RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
     RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
+    // CFG: every batch row reads xt/ctx row 0 (Bx = 1) at one broadcast t, so the rows are
+    // identical until the first cross-attention — proj_in and layer 0's self-attention
+    // block run on row 0 only and are copied (ACEHIP_DIT_DEDUP=0 disables, for A/B)
+    const char *de = getenv("ACEHIP_DIT_DEDUP");
+    const bool dup = Bx == 1 && Bc > 1 && t_stride == 0 && !(de && de[0] == '0');
     if (!h->graph_on || h->prof) {
-        RUN(forward_body(h, Bc, S, s));
+        RUN(forward_body(h, Bc, S, dup, s));
     } else {
-        const int key[4] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc)};
+        const int key[5] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), dup ? 1 : 0};
         if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
             if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
             if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
             HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
-            const int brc = forward_body(h, Bc, S, h->cap_stream);
+            const int brc = forward_body(h, Bc, S, dup, h->cap_stream);
             hipGraph_t g = nullptr;
             const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
             if (brc) { if (g) (void)hipGraphDestroy(g); return brc; }
@@ -543,7 +548,7 @@ int acehip_dit_set_graph(acehip_dit *h, int enable) {
 
 // Everything of one forward between the input packing and proj_out: reads only handle
 // buffers (emb, Xin, weights, K/V cache), so it can be captured once and replayed.
-static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s) {
+static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s) {
     const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L, M = Bc * S;
     const int H = h->cfg.heads, KV = h->cfg.kv_heads, Le = h->cond_Lenc;
     const float eps = h->cfg.eps, scale = 1.0f / sqrtf((float)h->cfg.head_dim);
@@ -563,7 +568,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s) {
     // proj_in (base:1347-1358) over the packed patches Xin
     GemmArgs g{};
     g.A = h->Xin; g.lda = 384; g.W = h->win; g.ldw = 384; g.C = h->X; g.ldc = D;
-    g.M = M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
+    g.M = dup ? S : M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
     RUN(hgemm(h, g, s));
 
     const size_t cper = (size_t)Bc * kvd * Le;
@@ -572,25 +577,28 @@ static int forward_body(acehip_dit *h, int Bc, int S, hipStream_t s) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
         const int64_t mbs = 6 * D;
-        // --- self-attention with AdaLN-Zero (base:499-511)
-        RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, M, D, eps, s));
+        // --- self-attention with AdaLN-Zero (base:499-511); layer 0 of identical CFG rows: row 0
+        const int Bs = (dup && l == 0) ? 1 : Bc, Ms = Bs * S;
+        RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, Ms, D, eps, s));
         // QKV projection with q/k RMSNorm + RoPE + head-major scatter fused in the epilogue
         GemmArgs q{};
         q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D;
-        q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_HEADPOST;
-        q.hp.B = Bc; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
+        q.M = Ms; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_HEADPOST;
+        q.hp.B = Bs; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
         RUN(timed(h, 2, s, [&] { return hgemm(h, q, s); }));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
-            return attention(h->Qh, h->Kh, h->Vh, h->AO, Bc, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
+            return attention(h->Qh, h->Kh, h->Vh, h->AO, Bs, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
                              scale, qd, h->attn_ws, s);
         }));
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
-        o.M = M; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
+        o.M = Ms; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
         RUN(timed(h, 3, s, [&] { return hgemm(h, o, s); }));
+        for (int b = Bs; b < Bc; ++b)
+            HIP_TRY(hipMemcpyAsync(h->X + (size_t)b * S * D, h->X, (size_t)S * D * 2, hipMemcpyDeviceToDevice, s));
         // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
         // rows, base:1907) get their constant cross-O output cnull[l] (set_uniform_rows)
         RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, Mq, D, eps, s));

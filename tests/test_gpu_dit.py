@@ -500,3 +500,34 @@ def test_gemm_tail_split(gpu_device, monkeypatch, M, N, K, epi):
         want, tol = ref, 5e-3
     assert rel_l2(on.cpu(), want.cpu()) < tol
     assert rel_l2(on.cpu(), off.cpu()) < tol
+
+
+def test_cfg_row_dedup_matches_full(gpu_device, monkeypatch):
+    """CFG rows reading the same xt/ctx row at one broadcast t are identical until the first
+    cross-attention: proj_in + layer 0's self-attention run on row 0 and are copied
+    (ACEHIP_DIT_DEDUP).  Same result as computing both rows (kernel rounding aside)."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=4, window=16)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=6, mode="parity").items()}
+    g = torch.Generator().manual_seed(21)
+    rt = DiTRuntime(cfg, 0, max_S=256, max_Bc=2, max_Lenc=64)
+    rt.load(W)
+    xt = torch.randn(1, 401, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(1, 401, 128, generator=g).bfloat16().to(gpu_device)
+    enc = torch.randn(2, 50, cfg.hidden_size, generator=g).bfloat16().to(gpu_device)
+    rt.set_condition(enc)
+    t = torch.tensor([0.7], dtype=torch.float32, device=gpu_device)
+    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
+    full = rt.forward(xt, ctx, t).float().clone()
+    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "1")
+    dd = rt.forward(xt, ctx, t).float()
+    torch.cuda.synchronize()
+    assert rel_l2(dd.cpu(), full.cpu()) < 2e-3
+    # a per-row t (t_stride 1) must not take the shortcut: rows then differ
+    t2 = torch.tensor([0.7, 0.3], dtype=torch.float32, device=gpu_device)
+    a = rt.forward(xt, ctx, t2).float()
+    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
+    b = rt.forward(xt, ctx, t2).float()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    rt.close()
