@@ -571,6 +571,8 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s) {
     g.M = dup ? S : M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
     RUN(hgemm(h, g, s));
 
+    const char *fe = getenv("ACEHIP_FUSE_ROWADD");
+    const bool fuse_rowadd = !(fe && fe[0] == '0');
     const size_t cper = (size_t)Bc * kvd * Le;
     const int Bq = std::min(h->uniform_from, Bc), Mq = Bq * S;   // rows with a real cross-attention
     for (int l = 0; l < L; ++l) {
@@ -616,9 +618,14 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s) {
         co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
         co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
         RUN(timed(h, 3, s, [&] { return hgemm(h, co, s); }));
-        if (Mq < M) RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
-        // --- SwiGLU MLP with AdaLN-Zero (base:528-533)
-        RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s));
+        // --- SwiGLU MLP with AdaLN-Zero (base:528-533); the null rows' constant cross-O output
+        // is added inside the norm pass (ACEHIP_FUSE_ROWADD=0: separate add_row_bcast, A/B)
+        RowAdd ra{};
+        if (Mq < M) {
+            if (fuse_rowadd) ra = RowAdd{h->X, h->cnull + (size_t)l * D, Mq};
+            else RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
+        }
+        RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s, ra));
         GemmArgs gu{};
         gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
         gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;

@@ -76,9 +76,16 @@ int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16
 //   plain: bf16(w · bf16(x·rsqrt(mean x²+eps)))
 //   mod:   bf16(bf16(plain · bf16(1+scale[b])) + shift[b])
 void rmsnorm_set_rows(int rows_per_wave);   // 0 = default
+// optional row add fused into rmsnorm_mod: rows >= from first become x = bf16(x + v[D]),
+// written back to xw (== x)
+struct RowAdd {
+    bf16_t *xw = nullptr;
+    const bf16_t *v = nullptr;
+    int from = 0;
+};
 int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
-                hipStream_t s);
+                hipStream_t s, RowAdd ra = RowAdd{});
 int head_post(const HeadPostArgs &a, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---

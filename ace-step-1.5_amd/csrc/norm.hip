@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
                                                           const bf16_t *__restrict__ scale,
                                                           int64_t mod_bstride, int rows_per_batch,
                                                           bf16_t *__restrict__ out, int M, int D,
-                                                          float eps) {
+                                                          float eps, RowAdd ra) {
     typedef typename VecOf<V>::T vec_t;
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
@@ -55,6 +55,26 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restri
         const bf16_t *xp = x + (int64_t)min(row0 + r, M - 1) * D;
 #pragma unroll
         for (int i = 0; i < NV; ++i) xr[r][i] = *(const vec_t *)(xp + (i * 64 + lane) * V);
+    }
+    // rows >= ra.from first get x = bf16(x + v), written back (the CFG null rows' constant
+    // cross-attention output, add_row_bcast folded into this pass)
+    if (ra.v) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = row0 + r;
+            if (row >= M || row < ra.from) continue;   // wave-uniform
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int e = (i * 64 + lane) * V;
+                float xv[V], av[V];
+                unpackv<V>(xr[r][i], xv);
+                unpackv<V>(*(const vec_t *)(ra.v + e), av);
+#pragma unroll
+                for (int j = 0; j < V; ++j) xv[j] += av[j];
+                xr[r][i] = packv<V>(xv);
+                *(vec_t *)(ra.xw + (int64_t)row * D + e) = xr[r][i];
+            }
+        }
     }
     // weight / modulation loads are independent of the reductions: issue them first
     vec_t wr[NV], s1r[NV], s2r[NV];
@@ -218,10 +238,10 @@ void rmsnorm_set_rows(int r) { g_rms_rows = r; }
 
 template <int R>
 static void rms_launch(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
-                       int64_t mbs, int rpb, bf16_t *out, int M, int D, float eps, hipStream_t s) {
+                       int64_t mbs, int rpb, bf16_t *out, int M, int D, float eps, RowAdd ra, hipStream_t s) {
     const int grid = (M + 4 * R - 1) / (4 * R);
 #define RMS_LAUNCH(V_, NV_) \
-    rmsnorm_mod_kernel<V_, NV_, R><<<grid, 256, 0, s>>>(x, w, shift, scale, mbs, rpb, out, M, D, eps)
+    rmsnorm_mod_kernel<V_, NV_, R><<<grid, 256, 0, s>>>(x, w, shift, scale, mbs, rpb, out, M, D, eps, ra)
     if (D % 512 == 0) {
         switch (D / 512) {
             case 1: RMS_LAUNCH(8, 1); break;
@@ -250,13 +270,14 @@ static void rms_launch(const bf16_t *x, const bf16_t *w, const bf16_t *shift, co
 
 int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
-                hipStream_t s) {
+                hipStream_t s, RowAdd ra) {
     if (M <= 0) return 0;
+    if (ra.v && (!ra.xw || ra.xw != x)) return fail(-1, "rmsnorm: row add must write back to x");
     if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
     if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
     const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
     const int R = g_rms_rows ? g_rms_rows : 1;
-    if (R < 0 && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
+    if (R < 0 && !ra.v && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
         const int WPR = -R, nv = D / (512 * WPR), grid = (M + 4 / WPR - 1) / (4 / WPR);
 #define SPLIT(NV_, W_) \
     rmsnorm_split_kernel<NV_, W_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps)
@@ -270,9 +291,9 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
         return 0;
     }
     switch (R < 0 ? 1 : R) {
-        case 1: rms_launch<1>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
-        case 2: rms_launch<2>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
-        default: rms_launch<4>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, s); break;
+        case 1: rms_launch<1>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, ra, s); break;
+        case 2: rms_launch<2>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, ra, s); break;
+        default: rms_launch<4>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, ra, s); break;
     }
     HIP_TRY(hipGetLastError());
     return 0;

@@ -531,3 +531,29 @@ def test_cfg_row_dedup_matches_full(gpu_device, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     rt.close()
+
+
+def test_null_row_add_fused_into_norm(gpu_device, monkeypatch):
+    """The CFG null rows' constant cross-O output added inside the MLP RMSNorm pass
+    (RowAdd) is bit-identical to the separate add_row_bcast launch."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=4, window=8)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=8, mode="parity").items()}
+    g = torch.Generator().manual_seed(13)
+    rt = DiTRuntime(cfg, 0, max_S=128, max_Bc=4, max_Lenc=40)
+    rt.load(W)
+    B, T, Le = 2, 203, 33
+    xt = torch.randn(B, T, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(B, T, 128, generator=g).bfloat16().to(gpu_device)
+    enc = torch.randn(B, Le, cfg.hidden_size, generator=g).bfloat16()
+    null = torch.randn(1, 1, cfg.hidden_size, generator=g).bfloat16()
+    rt.set_condition(torch.cat([enc, null.expand_as(enc)]).to(gpu_device))
+    rt.set_uniform_rows(B)
+    t = torch.tensor([0.4], dtype=torch.float32, device=gpu_device)
+    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "0")
+    sep = rt.forward(xt, ctx, t).clone()
+    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "1")
+    fused = rt.forward(xt, ctx, t)
+    torch.cuda.synchronize()
+    assert torch.equal(sep, fused)
+    rt.close()
