@@ -18,6 +18,7 @@ fallback (``_ffi.lib()`` raises if the library is absent).
 """
 from __future__ import annotations
 
+import inspect
 import math
 import time
 from typing import Dict, List, Optional, Union
@@ -228,16 +229,29 @@ def turbo_schedule(shift=3.0, timesteps=None) -> List[float]:
     return sched
 
 
+def takes_timesteps(model) -> bool:
+    """base vs sft share one config; they are told apart by ``generate_audio``'s
+    signature: sft declares ``timesteps`` (sft:1811), base swallows it in ``**kwargs``."""
+    try:
+        return "timesteps" in inspect.signature(model.generate_audio).parameters
+    except (TypeError, ValueError):
+        return False
+
+
 class AceStepDiTBackend:
     """Drop-in for ``AceStepConditionGenerationModel.generate_audio``."""
 
     def __init__(self, runtime: DiTRuntime, null_condition_emb: torch.Tensor, is_turbo: bool = False,
-                 prepare_condition=None, dtype=torch.bfloat16):
+                 prepare_condition=None, dtype=torch.bfloat16, accepts_timesteps: Optional[bool] = None):
         self.rt = runtime
         self.device = runtime.device
         self.dtype = dtype
         self.null = null_condition_emb.detach().to(self.device, dtype)
         self.is_turbo = is_turbo
+        # custom ``timesteps``: the turbo (turbo:1803,1828-1857) and sft (sft:1811,1866-1868)
+        # samplers honour them; base has no such parameter and swallows it in **kwargs
+        # (base:1812), so a base checkpoint ignores it.  None = the turbo default (base).
+        self.accepts_timesteps = is_turbo if accepts_timesteps is None else bool(accepts_timesteps)
         self.prepare_condition = prepare_condition
         self.uniform_null = True     # closed-form cross-attention for the CFG null rows
 
@@ -261,7 +275,8 @@ class AceStepDiTBackend:
         rt.load(model.decoder.state_dict())
         turbo = bool(getattr(c, "is_turbo", False)) or getattr(c, "model_version", "") == "turbo"
         return cls(rt, model.null_condition_emb, is_turbo=turbo,
-                   prepare_condition=model.prepare_condition, dtype=next(model.parameters()).dtype)
+                   prepare_condition=model.prepare_condition, dtype=next(model.parameters()).dtype,
+                   accepts_timesteps=turbo or takes_timesteps(model))
 
     # ------------------------------------------------------------------ API --
     def _condition(self, kw):
@@ -342,7 +357,8 @@ class AceStepDiTBackend:
         shift = float(kw.get("shift", 1.0))
         method = kw.get("infer_method", "ode")
         use_adg = bool(kw.get("use_adg", False))
-        t = base_schedule(infer_steps, shift, device, dtype, kw.get("timesteps"))
+        t = base_schedule(infer_steps, shift, device, dtype,
+                          kw.get("timesteps") if self.accepts_timesteps else None)
         noise = prepare_noise((B, T, ctx.shape[-1] // 2), device, dtype, kw.get("seed"))
         cns = float(kw.get("cover_noise_strength", 0.0))
         if cns > 0.0:

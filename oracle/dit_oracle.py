@@ -38,7 +38,7 @@ def timestep_embedding(W: Dict[str, Tensor], prefix: str, t: Tensor,
     parity-critical detail of SURVEY §8a a7); the sinusoid is fp32."""
     ts = t * scale
     half = n_freq // 2
-    freqs = torch.exp(-math.log(10000) * torch.arange(0, half, dtype=torch.float32) / half)
+    freqs = torch.exp(-math.log(10000) * torch.arange(0, half, dtype=torch.float32) / half).to(t.device)
     args = ts[:, None].float() * freqs[None]
     emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
     h = F.linear(emb.to(t.dtype), W[f"{prefix}.linear_1.weight"], W[f"{prefix}.linear_1.bias"])
@@ -48,7 +48,7 @@ def timestep_embedding(W: Dict[str, Tensor], prefix: str, t: Tensor,
     return temb, proj.unflatten(1, (6, -1))
 
 
-def rope_tables(S: int, head_dim: int, theta: float, dtype) -> Tuple[Tensor, Tensor]:
+def rope_tables(S: int, head_dim: int, theta: float, dtype, device="cpu") -> Tuple[Tensor, Tensor]:
     """Qwen3RotaryEmbedding default init + forward (modeling_qwen3.py:116-137):
     fp32 inv_freq, positions 0..S-1, cat(freqs,freqs), cos/sin cast to dtype.
 
@@ -57,8 +57,8 @@ def rope_tables(S: int, head_dim: int, theta: float, dtype) -> Tuple[Tensor, Ten
     ``inv_freq`` buffer: in bf16 mode the frequencies are bf16-rounded before
     the fp32 outer product."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float) / head_dim))
-    inv = inv.to(dtype).float()
-    pos = torch.arange(S, dtype=torch.float32)
+    inv = inv.to(dtype).float().to(device)
+    pos = torch.arange(S, dtype=torch.float32, device=device)
     freqs = (inv[None, :, None] @ pos[None, None, :]).transpose(1, 2)   # [1,S,hd/2]
     emb = torch.cat((freqs, freqs), dim=-1)
     return emb.cos().to(dtype), emb.sin().to(dtype)
@@ -69,16 +69,16 @@ def _rotate_half(x: Tensor) -> Tensor:
     return torch.cat((-x[..., h:], x[..., :h]), dim=-1)
 
 
-def additive_mask(S_q: int, S_k: int, dtype, window: Optional[int]) -> Tensor:
+def additive_mask(S_q: int, S_k: int, dtype, window: Optional[int], device="cpu") -> Tensor:
     """create_4d_mask (base:56-135) for the decoder's bidirectional case with
     no padding mask (the decoder forces padding masks to None, base:1384-1385):
     0 where |i-j| <= window (or everywhere for full/cross), finfo.min elsewhere."""
     n = max(S_q, S_k)
-    idx = torch.arange(n)
-    valid = torch.ones(n, n, dtype=torch.bool)
+    idx = torch.arange(n, device=device)
+    valid = torch.ones(n, n, dtype=torch.bool, device=device)
     if window is not None:
         valid = (idx[:, None] - idx[None, :]).abs() <= window
-    m = torch.full((1, 1, n, n), torch.finfo(dtype).min, dtype=dtype)
+    m = torch.full((1, 1, n, n), torch.finfo(dtype).min, dtype=dtype, device=device)
     m.masked_fill_(valid[None, None], 0.0)
     return m[:, :, :S_q, :S_k]
 
@@ -143,10 +143,11 @@ def dit_forward(W: Dict[str, Tensor], cfg, xt: Tensor, t: Tensor, t_r: Tensor,
         kv_cache = cross_kv(W, cfg, enc)
     B, S, D = h.shape
     Lenc = kv_cache[0][0].shape[2]
-    full_mask = additive_mask(S, S, dt, None)
-    band_mask = additive_mask(S, S, dt, cfg.sliding_window)
-    enc_mask = additive_mask(S, Lenc, dt, None)
-    cos, sin = rope_tables(S, hd, cfg.rope_theta, dt)
+    dev = xt.device      # the oracle also runs as torch-on-device for the full-length checks
+    full_mask = additive_mask(S, S, dt, None, dev)
+    band_mask = additive_mask(S, S, dt, cfg.sliding_window, dev)
+    enc_mask = additive_mask(S, Lenc, dt, None, dev)
+    cos, sin = rope_tables(S, hd, cfg.rope_theta, dt, dev)
     cos, sin = cos.unsqueeze(1), sin.unsqueeze(1)
 
     for i in range(cfg.num_hidden_layers):

@@ -142,13 +142,15 @@ def _runtime(cfg, W, gpu_device, max_S=64, max_Bc=2, max_Lenc=32):
     return rt
 
 
-@pytest.mark.parametrize("name", ["tiny_bfloat16", "tiny_odd_bfloat16", "full2_bfloat16"])
+@pytest.mark.parametrize("name", ["tiny_bfloat16", "tiny_odd_bfloat16", "full2_bfloat16",
+                                  # full width, T = 641 (S = 321 > 2W+1: the ±128 band is pinned)
+                                  "full2_long_bfloat16"])
 def test_dit_forward_vs_reference_golden(gpu_device, name):
     meta = golden_manifest()["forward"][name]
     cfg = DiTConfig(**meta["cfg"])
     g = load_golden("dit_fwd_" + name)
     W = synth_dit_weights(cfg, seed=meta["seed"], mode="parity")
-    rt = _runtime(cfg, W, gpu_device)
+    rt = _runtime(cfg, W, gpu_device, max_S=max(64, (meta["T"] + 1) // 2), max_Lenc=max(32, meta["Lenc"]))
     rt.set_condition(g["enc"].to(gpu_device))
     out = rt.forward(g["xt"].to(gpu_device).contiguous(), g["ctx"].to(gpu_device).contiguous(),
                      g["t"].float().to(gpu_device), g["t_r"].float().to(gpu_device))

@@ -1,0 +1,174 @@
+"""Full-length parity: the long-sequence regimes configs 2/4/5 exist for
+(240 s → T = 6000 / S = 3000, 600 s → T = 15000 / S = 7500).
+
+* DiT: 2-layer full-width forwards (one band ±128 layer, one full layer) at
+  S = 3000 and S = 7500 with the production CFG layout (Bx = 1, Bc = 2, null
+  rows in closed form, layer-0 row dedup, null-row add fused in the norm pass)
+  against the oracle run as torch on the same device (rocBLAS / SDPA, not our
+  kernels) in bf16 — the reference's GPU precision — tolerance §8c(ii):
+  rel-L2 <= 2.5 %, cosine >= 0.999.
+* Attention at S = 7500 (full, band, cross over Lenc = 641) against an fp32
+  torch softmax attention, query-chunked.
+* VAE decode of a whole 240 s / 600 s latent sequence, untiled: (a) windows at
+  the start, middle and end are bit-identical to decoding that window alone
+  (the decoder's receptive field is −8.2/+9.2 frames, SURVEY §8a a19, so
+  overlap-discard tiling ≡ untiled — vae_decode_chunks.py:99-110 — and int64
+  addressing past 2³¹ elements at 600 s is exercised); (b) each window against
+  the fp32 CPU oracle (parity unpinned: diffusers is absent).
+* VAE encode of a 240 s stereo source: same two checks on latent windows.
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import cosine, rel_l2
+
+from acehip.config import DiTConfig, VAEConfig
+from acehip.weights import synth_dit_weights, synth_null_condition, synth_vae_weights
+from oracle import dit_oracle, vae_oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL_REL, TOL_COS = 0.025, 0.999
+
+
+@pytest.fixture(scope="module")
+def dit2(gpu_device):
+    cfg = DiTConfig(num_hidden_layers=2)           # layer 0 band ±128, layer 1 full
+    assert cfg.is_sliding(0) and not cfg.is_sliding(1)
+    W = synth_dit_weights(cfg, seed=31, mode="parity")
+    Wd = {k: v.to(gpu_device, torch.bfloat16) for k, v in W.items()}
+    null = synth_null_condition(cfg, seed=32).to(gpu_device, torch.bfloat16)
+    return cfg, Wd, null
+
+
+@pytest.mark.parametrize("T", [6000, 15000])
+def test_dit_forward_full_length_cfg(gpu_device, dit2, T):
+    from acehip.dit import DiTRuntime
+    cfg, W, null = dit2
+    S, Lenc = (T + 1) // 2, 641
+    g = torch.Generator(device=gpu_device).manual_seed(T)
+    xt = torch.randn(1, T, 64, device=gpu_device, generator=g).bfloat16()
+    ctx = torch.randn(1, T, 128, device=gpu_device, generator=g).bfloat16()
+    ctx[..., 64:] = 1
+    enc = torch.randn(1, Lenc, cfg.hidden_size, device=gpu_device, generator=g).bfloat16()
+    enc2 = torch.cat([enc, null.reshape(1, 1, -1).expand_as(enc)]).contiguous()   # base:1907
+    t = torch.tensor([0.6328125], dtype=torch.float32, device=gpu_device)
+    rt = DiTRuntime(cfg, gpu_device.index or 0, max_S=S, max_Bc=2, max_Lenc=Lenc)
+    rt.load(W)
+    rt.set_condition(enc2)
+    rt.set_uniform_rows(1)                         # CFG null rows in closed form (production)
+    out = rt.forward(xt, ctx, t).float()
+    torch.cuda.synchronize()
+    rt.close()
+    with torch.no_grad():
+        tb = t.bfloat16().expand(2)
+        ref = dit_oracle.dit_forward(W, cfg, torch.cat([xt, xt]), tb, tb, enc2, torch.cat([ctx, ctx])).float()
+    assert out.shape == ref.shape == (2, T, 64)
+    for b in range(2):                              # conditional row and the null row separately
+        r, c = rel_l2(out[b].cpu(), ref[b].cpu()), cosine(out[b].cpu(), ref[b].cpu())
+        assert r <= TOL_REL and c >= TOL_COS, (T, b, r, c)
+
+
+def _attn_ref_chunked(q, k, v, window, chunk=1024):
+    """fp32 softmax(QKᵀ/√128 + band mask)·V, query-chunked (S×S never whole)."""
+    B, H, Sq, _ = q.shape
+    rep = H // k.shape[1]
+    kf = k.float().repeat_interleave(rep, 1)
+    vf = v.float().repeat_interleave(rep, 1)
+    out = torch.empty(B, H, Sq, 128, device=q.device)
+    j = torch.arange(k.shape[2], device=q.device)[None, :]
+    for s0 in range(0, Sq, chunk):
+        qs = q[:, :, s0:s0 + chunk].float()
+        s = (qs @ kf.transpose(2, 3)) / math.sqrt(128)
+        if window >= 0:
+            i = torch.arange(s0, s0 + qs.shape[2], device=q.device)[:, None]
+            s = s.masked_fill((i - j).abs() > window, float("-inf"))
+        out[:, :, s0:s0 + chunk] = torch.softmax(s, -1) @ vf
+    return out.transpose(1, 2).reshape(B, Sq, H * 128)
+
+
+@pytest.mark.parametrize("Sq,Sk,window", [(7500, 7500, -1), (7500, 7500, 128), (7500, 641, -1)])
+def test_attention_s7500(gpu_device, Sq, Sk, window):
+    from acehip import _ffi as ff
+    B, H, KV = 2, 16, 8
+    g = torch.Generator(device=gpu_device).manual_seed(Sq + Sk + window)
+    q = torch.randn(B, H, Sq, 128, device=gpu_device, generator=g).bfloat16()
+    k = torch.randn(B, KV, Sk, 128, device=gpu_device, generator=g).bfloat16()
+    v = torch.randn(B, KV, Sk, 128, device=gpu_device, generator=g).bfloat16()
+    o = torch.empty(B, Sq, H * 128, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, Sq, Sk, window,
+                                            1 / math.sqrt(128), ff.stream_ptr()))
+    torch.cuda.synchronize()
+    ref = _attn_ref_chunked(q, k, v, window)
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 1e-2
+
+
+@pytest.fixture(scope="module")
+def vae_full(gpu_device):
+    from acehip.vae import OobleckBackend
+    cfg = VAEConfig()
+    W = synth_vae_weights(cfg, seed=5, mode="parity", with_encoder=True)
+    be = OobleckBackend(cfg, gpu_device.index or 0, max_T=15000, with_encoder=True)
+    be.load({k: v.to(gpu_device) for k, v in W.items()})
+    yield cfg, W, be
+    be.close()
+
+
+CORE, CTX = 32, 40        # frames compared / frames of context each side (> receptive field 9.2)
+# fp32 oracle vs the bf16 HIP path: the restatement's own bf16-vs-fp32 spread at the full
+# config is 7.8 % rel-L2 (test_vae.py calibration); the window check allows that spread + 2 %
+VAE_WIN_TOL = 0.10
+
+
+def _windows(T):
+    return [0, T // 2 - CORE // 2, T - CORE]
+
+
+@pytest.mark.parametrize("T", [6000, 15000])
+def test_vae_decode_full_length_windows(gpu_device, vae_full, T):
+    cfg, W, be = vae_full
+    hop = cfg.hop_length
+    g = torch.Generator(device=gpu_device).manual_seed(T + 1)
+    z = torch.randn(1, 64, T, device=gpu_device, generator=g).bfloat16()
+    wav = be.decode_tensor(z)                        # untiled, [1, 2, T·1920] fp32
+    torch.cuda.synchronize()
+    assert wav.shape == (1, 2, T * hop) and torch.isfinite(wav).all()
+    for c0 in _windows(T):
+        lo, hi = max(0, c0 - CTX), min(T, c0 + CORE + CTX)
+        win = be.decode_tensor(z[:, :, lo:hi].contiguous())
+        torch.cuda.synchronize()
+        a = wav[:, :, c0 * hop:(c0 + CORE) * hop]
+        b = win[:, :, (c0 - lo) * hop:(c0 - lo + CORE) * hop]
+        assert torch.equal(a, b), (T, c0, (a - b).abs().max().item())      # tiled ≡ untiled, bit for bit
+        with torch.no_grad():
+            ref = vae_oracle.decode(W, cfg, z[:, :, lo:hi].float().cpu())[:, :, (c0 - lo) * hop:(c0 - lo + CORE) * hop]
+        r, c = rel_l2(a.cpu(), ref), cosine(a.cpu(), ref)
+        assert r <= VAE_WIN_TOL and c >= 0.995, (T, c0, r, c)
+
+
+def test_vae_encode_full_length_windows(gpu_device, vae_full):
+    cfg, W, be = vae_full
+    T, hop = 6000, cfg.hop_length
+    g = torch.Generator(device=gpu_device).manual_seed(7)
+    n = T * hop
+    tt = torch.arange(n, device=gpu_device, dtype=torch.float32) / 48000.0
+    sw = torch.sin(2 * math.pi * 220.0 * tt) + 0.5 * torch.sin(2 * math.pi * 523.25 * tt + 1.9)
+    wav = (0.25 * torch.stack([sw, torch.roll(sw, 480)])[None]
+           + 0.05 * torch.randn(1, 2, n, device=gpu_device, generator=g)).bfloat16().contiguous()
+    del sw, tt
+    z = be.encode_tensor(wav, sample=False)          # the mean, [1, 64, T]
+    torch.cuda.synchronize()
+    assert z.shape == (1, 64, T) and torch.isfinite(z.float()).all()
+    for c0 in _windows(T):
+        lo, hi = max(0, c0 - CTX), min(T, c0 + CORE + CTX)
+        zw = be.encode_tensor(wav[:, :, lo * hop:hi * hop].contiguous(), sample=False)
+        torch.cuda.synchronize()
+        a = z[:, :, c0:c0 + CORE]
+        b = zw[:, :, c0 - lo:c0 - lo + CORE]
+        assert torch.equal(a, b), (c0, (a.float() - b.float()).abs().max().item())
+        with torch.no_grad():
+            ref = vae_oracle.encode_sample(W, cfg, wav[:, :, lo * hop:hi * hop].float().cpu())[:, :, c0 - lo:c0 - lo + CORE]
+        r = rel_l2(a.float().cpu(), ref)
+        assert r < 0.03, (c0, r)

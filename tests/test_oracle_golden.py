@@ -16,7 +16,8 @@ def _cfg(meta):
 
 
 @pytest.mark.parametrize("name", ["tiny_float32", "tiny_odd_float32", "tiny_bfloat16",
-                                  "tiny_odd_bfloat16", "full2_float32", "full2_bfloat16"])
+                                  "tiny_odd_bfloat16", "full2_float32", "full2_bfloat16",
+                                  "full2_long_float32", "full2_long_bfloat16"])
 def test_dit_forward_matches_reference(name):
     meta = golden_manifest()["forward"][name]
     cfg = _cfg(meta)

@@ -62,7 +62,8 @@ def _import_ref(variant: str):
     sys.path.insert(0, d)
     try:
         import configuration_acestep_v15 as C
-        mod = __import__(f"modeling_acestep_v15_{variant}")
+        # the sft variant ships its modeling file under the base name
+        mod = __import__(f"modeling_acestep_v15_{'base' if variant == 'sft' else variant}")
     finally:
         sys.path.remove(d)
     return C, mod
@@ -164,20 +165,43 @@ def gen_sampler(variant, name, dtype, B, T, **gen_kw):
         silence_latent=torch.randn(1, T, 64, generator=g).to(dtype),
         seed=list(range(B)), use_progress_bar=False,
     )
+    if gen_kw.get("audio_cover_strength", 1.0) < 1.0:
+        kw["non_cover_text_hidden_states"] = torch.randn(B, Lt, 1024, generator=g).to(dtype)
+        kw["non_cover_text_attention_mask"] = torch.ones(B, Lt, dtype=torch.long)
     kw.update(gen_kw)
-    with torch.no_grad():
-        res = model.generate_audio(**kw)
+    # the SDE branch re-noises with the unseeded global RNG (base:1777 randn_like,
+    # turbo:1984): record every draw so a replay can inject the same noise
+    noise_draws = []
+    orig_randn_like = torch.randn_like
+
+    def randn_like(x, *a, **k):
+        n = orig_randn_like(x, *a, **k)
+        noise_draws.append(n.clone())
+        return n
+    torch.randn_like = randn_like
+    try:
+        with torch.no_grad():
+            res = model.generate_audio(**kw)
+    finally:
+        torch.randn_like = orig_randn_like
     tensors = {"target_latents": res["target_latents"].contiguous()}
     for i, (x, t, v, e, c) in enumerate(rec.calls):
         tensors[f"x_{i}"] = x
         tensors[f"t_{i}"] = t
         tensors[f"vt_{i}"] = v
-    tensors["enc"] = rec.calls[0][3]
-    tensors["ctx"] = rec.calls[0][4]
+        tensors[f"enc_{i}"] = e
+        tensors[f"ctx_{i}"] = c
+    for i, n in enumerate(noise_draws):
+        tensors[f"noise_{i}"] = n
+    tensors["enc"] = rec.calls[0][3].clone()
+    tensors["ctx"] = rec.calls[0][4].clone()
+    tensors["src_latents"] = kw["src_latents"].clone()
+    tensors["silence_latent"] = kw["silence_latent"].clone()
     save_file(tensors, os.path.join(OUT, f"sampler_{name}.safetensors"))
-    meta = {k: (v if isinstance(v, (int, float, str, bool, list)) else None) for k, v in gen_kw.items()}
+    meta = {k: (v if isinstance(v, (int, float, str, bool, list)) else
+                (v.tolist() if isinstance(v, torch.Tensor) else None)) for k, v in gen_kw.items()}
     return {"variant": variant, "dtype": str(dtype), "B": B, "T": T, "n_calls": len(rec.calls),
-            "kwargs": meta}
+            "n_noise": len(noise_draws), "kwargs": meta}
 
 
 def gen_adg_direct(name, B, T, seed, sigmas, guidance):
@@ -319,6 +343,36 @@ def main_only(which):
         manifest["sampler"]["base_s8_adg"] = gen_sampler("base", "base_s8_adg", bf, 1, 40, infer_steps=8,
                                                          shift=3.0, diffusion_guidance_sale=7.0,
                                                          use_adg=True)
+    if "sampler2" in which:
+        # the branches round 1 left without a GPU replay: cover-noise truncation
+        # (base:1879-1902, turbo:1922-1936), the cover -> non-cover switch
+        # (base:1836-1856,1916-1927; turbo:1892-1956), SDE re-noise (base:1968-1973,
+        # turbo:1980-1984) with the unseeded draws recorded, sft custom timesteps
+        # (sft:1866-1868)
+        sm = manifest["sampler"]
+        sm["base_s8_cover"] = gen_sampler("base", "base_s8_cover", bf, 2, 40, infer_steps=8, shift=3.0,
+                                          diffusion_guidance_sale=7.0, cover_noise_strength=0.35)
+        sm["base_s8_acs"] = gen_sampler("base", "base_s8_acs", bf, 1, 40, infer_steps=8, shift=3.0,
+                                        diffusion_guidance_sale=7.0, audio_cover_strength=0.5)
+        sm["base_s8_sde"] = gen_sampler("base", "base_s8_sde", bf, 2, 40, infer_steps=8, shift=3.0,
+                                        diffusion_guidance_sale=7.0, infer_method="sde")
+        sm["base_s10_cover_acs_sde"] = gen_sampler("base", "base_s10_cover_acs_sde", bf, 1, 32, infer_steps=10,
+                                                   shift=2.0, diffusion_guidance_sale=5.0, cover_noise_strength=0.5,
+                                                   audio_cover_strength=0.6, infer_method="sde")
+        sm["turbo_cover_acs"] = gen_sampler("turbo", "turbo_cover_acs", bf, 1, 40, shift=3.0,
+                                            cover_noise_strength=0.3, audio_cover_strength=0.5)
+        sm["turbo_sde"] = gen_sampler("turbo", "turbo_sde", bf, 2, 40, shift=1.0, infer_method="sde")
+        sm["sft_timesteps"] = gen_sampler("sft", "sft_timesteps", bf, 1, 40, diffusion_guidance_sale=7.0,
+                                          shift=3.0, timesteps=torch.tensor([1.0, 0.9, 0.7, 0.5, 0.3, 0.1, 0.0]))
+    if "long" in which:
+        # full width with S > 2W+1 so the ±128 band of the even layers is pinned at full
+        # width against the reference (base:56-135, :1378-1447); odd T (pad + crop)
+        full2 = DiTConfig(num_hidden_layers=2)
+        C, M = _import_ref("base")
+        for dt in (torch.float32, torch.bfloat16):
+            tag = str(dt).split(".")[-1]
+            manifest["forward"][f"full2_long_{tag}"] = gen_forward(M, C, f"full2_long_{tag}", full2, 2, 641, 48, dt,
+                                                                  22, [0.5, 0.5], [0.5, 0.5])
     if "tokenizer" in which:
         manifest["tokenizer"] = {f"tiny_{str(dt).split('.')[-1]}": gen_tokenizer(f"tiny_{str(dt).split('.')[-1]}", dt, 41)
                                  for dt in (torch.float32, torch.bfloat16)}
