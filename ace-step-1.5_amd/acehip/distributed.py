@@ -14,6 +14,11 @@ Scaling is therefore "weak": per-GPU work is fixed as the node grows.
 from __future__ import annotations
 
 import os
+import signal
+import socket
+import subprocess
+import sys
+import time
 from typing import List, Optional, Sequence
 
 import torch
@@ -23,6 +28,59 @@ import torch.distributed as dist
 def env_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), \
         int(os.environ.get("LOCAL_RANK", 0))
+
+
+def needs_launch(n_procs: int) -> bool:
+    """True when ``n_procs`` > 1 ranks are asked for but this process was not
+    started by a launcher (no WORLD_SIZE in the environment)."""
+    return n_procs > 1 and "WORLD_SIZE" not in os.environ
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_local(argv: Sequence[str], n_procs: int, extra_env: Optional[dict] = None,
+                 timeout: Optional[float] = None) -> int:
+    """Start ``n_procs`` ranks of ``python argv...`` on this node — one process per
+    GPU, the torchrun environment contract (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) — and wait for all.
+
+    Must be called before anything touches the GPU (the children are fresh
+    interpreters started with subprocess, never exec).  If a rank fails, the
+    remaining ranks are terminated (by their exact PIDs) and its exit code is
+    returned; 0 when every rank succeeded."""
+    port = _free_port()
+    procs = []
+    for r in range(n_procs):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n_procs),
+                    "LOCAL_WORLD_SIZE": str(n_procs), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable, *argv], env=env))
+    deadline = None if timeout is None else time.time() + timeout
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:                 # one rank died: end the others
+                    q.send_signal(signal.SIGTERM)
+        if deadline is not None and time.time() > deadline and live:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+            deadline = None
+        time.sleep(0.05)
+    return rc
 
 
 def init(backend: Optional[str] = None, device: Optional[torch.device] = None):
@@ -66,6 +124,21 @@ def barrier(device: Optional[torch.device] = None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+def gather_floats(vals: Sequence[float], device: Optional[torch.device] = None) -> List[float]:
+    """All ranks' values, rank-major (all_gather; the caller's own list at world 1)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in vals]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x) for o in out for x in o.tolist()]
+
+
+def destroy():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def gather_to_rank0(t: torch.Tensor) -> Optional[List[torch.Tensor]]:

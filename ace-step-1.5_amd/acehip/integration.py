@@ -11,7 +11,13 @@ Seams:
              reference's own ``prepare_condition`` for the conditioning.
   * VAE    — ``handler.vae.decode(z).sample`` (``vae_decode_chunks.py:42,95``)
              and ``handler.vae.encode(x).latent_dist.sample()``
-             (``vae_encode.py:65``): replaced by :class:`~acehip.vae.OobleckBackend`.
+             (``vae_encode.py:65``): replaced by :class:`~acehip.vae.OobleckBackend`;
+             ``handler.tiled_decode`` (``vae_decode.py:16-85``, called at
+             ``generate_music_decode.py:164``) becomes ONE untiled decode of the
+             whole batch — the reference's overlap-discard windows (1.6x the useful
+             frames at 240 s) are redundant because the decoder's receptive field
+             (-8.2/+9.2 frames) is inside the 64-frame overlap (tiled == untiled,
+             tests/test_gpu_long.py).
 
   * cond   — ``prepare_condition`` (``base:1607-1652``, called from
              ``generate_audio`` ``base:1820``): replaced by
@@ -45,7 +51,8 @@ from .vae import OobleckBackend
 log = logging.getLogger("acehip")
 
 
-def vae_from_diffusers(vae, max_seconds: float = 600.0, with_encoder: bool = True) -> OobleckBackend:
+def vae_from_diffusers(vae, max_seconds: float = 600.0, with_encoder: bool = True,
+                       max_batch: int = 8) -> OobleckBackend:
     """Build an OobleckBackend from a loaded diffusers ``AutoencoderOobleck``
     (precedent: ``acestep/models/mlx/vae_convert.py:37-132``)."""
     c = vae.config
@@ -55,7 +62,7 @@ def vae_from_diffusers(vae, max_seconds: float = 600.0, with_encoder: bool = Tru
                     decoder_input_channels=c.decoder_input_channels, audio_channels=c.audio_channels)
     dev = next(vae.parameters()).device
     be = OobleckBackend(cfg, dev.index or 0, max_T=int(max_seconds * 48000 / cfg.hop_length) + 1,
-                        with_encoder=with_encoder)
+                        max_B=max_batch, with_encoder=with_encoder)
     be.load(vae.state_dict())
     return be
 
@@ -124,8 +131,12 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
             tok.load({"tokenizer." + k: v for k, v in m.tokenizer.state_dict().items()})
             det = AudioDetokenizer(ce.cfg, dev, max_patches=max_batch * patches)
             det.load({"detokenizer." + k: v for k, v in m.detokenizer.state_dict().items()})
-        dit.prepare_condition = HipPrepareCondition(ce, fallback=m.prepare_condition, tokenizer=tok,
-                                                    detokenizer=det)
+        hip_prep = HipPrepareCondition(ce, fallback=m.prepare_condition, tokenizer=tok, detokenizer=det)
+        dit.prepare_condition = hip_prep
+        # the handler also calls prepare_condition itself before generate_audio
+        # (service_generate_execute.py:123-142); same contract, same HIP encoders
+        m.prepare_condition = hip_prep
+        out_prep = hip_prep
     orig_generate = handler.model.generate_audio
 
     def generate_audio(**kw):
@@ -139,6 +150,8 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
 
     handler.model.generate_audio = generate_audio
     out = {"dit": dit}
+    if condition:
+        out["prepare_condition"] = out_prep
 
     # LoRA lifecycle: after any adapter change re-pack the merged decoder weights
     for meth in _LORA_METHODS:
@@ -158,7 +171,7 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
         handler.text_encoder = te
         out["text_encoder"] = te
     if vae and getattr(handler, "vae", None) is not None:
-        vb = vae_from_diffusers(handler.vae, max_seconds=max_seconds)
+        vb = vae_from_diffusers(handler.vae, max_seconds=max_seconds, max_batch=max_batch)
         orig_decode, orig_encode = handler.vae.decode, handler.vae.encode
 
         def decode(z, *a, **k):
@@ -181,5 +194,38 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
 
         handler.vae.decode = decode
         handler.vae.encode = encode
+        orig_tiled = getattr(handler, "tiled_decode", None)
+
+        def tiled_decode(latents, chunk_size=None, overlap=64, offload_wav_to_cpu=None):
+            # vae_decode.py:16-85 contract: [B, 64, T] -> [B, 2, T*hop]; untiled here
+            try:
+                return vb.tiled_decode(latents, chunk_size, overlap, offload_wav_to_cpu)
+            except Exception as e:  # pragma: no cover
+                if not fallback or orig_tiled is None:
+                    raise
+                log.warning("acehip tiled_decode failed (%s); falling back", e)
+                return orig_tiled(latents, chunk_size=chunk_size, overlap=overlap,
+                                  offload_wav_to_cpu=offload_wav_to_cpu)
+        handler.tiled_decode = tiled_decode
         out["vae"] = vb
     return out
+
+
+def hip_normalize_audio(audio_data: torch.Tensor, target_db: float = -1.0) -> torch.Tensor:
+    """``normalize_audio`` (acestep/audio_utils.py:24-62) for device tensors: same
+    contract (returns a new tensor; silence returned unchanged) on the fused HIP
+    pass.  A caller that normalizes while the audio is still on the GPU (before the
+    payload's host copy) can bind it in place of the CPU pass at inference.py:679."""
+    if not (isinstance(audio_data, torch.Tensor) and audio_data.is_cuda):
+        raise TypeError("hip_normalize_audio: a GPU tensor is required (no CPU path)")
+    x = audio_data.detach().float().contiguous().clone().reshape(1, -1)
+    if x.shape[1] % 4:
+        raise ValueError("hip_normalize_audio: sample count must be a multiple of 4")
+    peak = torch.empty(1, device=x.device, dtype=torch.float32)
+    from ._ffi import check, lib, ptr, stream_ptr
+    target = float(torch.tensor(10 ** (target_db / 20.0), dtype=torch.float32))
+    if target_db > 0.0:
+        raise ValueError("hip_normalize_audio: target_db must be <= 0 (inference.py:674)")
+    # guard off: normalize_audio alone scales a peak above 1 in one multiply
+    check(lib().acehip_wav_postprocess(ptr(x), 1, x.shape[1], ptr(peak), 0, target, stream_ptr()), "wav_normalize")
+    return x.reshape(audio_data.shape).to(audio_data.dtype)

@@ -77,6 +77,25 @@ class OobleckBackend:
               "wav_peak_normalize")
         return wav
 
+    def postprocess_(self, wav: torch.Tensor, normalization_db: Optional[float] = -1.0) -> torch.Tensor:
+        """In place, one fused HIP pass pair per batch: the decode guard (divide a song by
+        its peak when > 1, generate_music_decode.py:193-195) followed by the product's
+        ``normalize_audio(audio, normalization_db)`` (audio_utils.py:24-62, applied at
+        inference.py:674-679 when ``enable_normalization and normalization_db <= 0``);
+        ``normalization_db=None`` = guard only.  Bit-identical to the two reference steps."""
+        assert wav.dtype == torch.float32 and wav.is_contiguous()
+        target = 0.0
+        if normalization_db is not None:
+            if normalization_db > 0.0:
+                raise ValueError("normalization_db must be <= 0 (inference.py:674)")
+            # torch promotes the python float to fp32 in target_amp / peak
+            target = float(torch.tensor(10 ** (normalization_db / 20.0), dtype=torch.float32))
+        B = wav.shape[0]
+        peak = torch.empty(B, device=wav.device, dtype=torch.float32)
+        check(lib().acehip_wav_postprocess(ptr(wav), B, wav.numel() // B, ptr(peak), 1, target, stream_ptr()),
+              "wav_postprocess")
+        return wav
+
     def decode(self, z: torch.Tensor):
         """diffusers-style: ``.decode(z).sample``."""
         return SimpleNamespace(sample=self.decode_tensor(z))

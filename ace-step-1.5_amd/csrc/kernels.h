@@ -115,7 +115,9 @@ int fsq_codes_from_indices(const int *idx, int M, const FsqLevels &lv, bf16_t *c
 
 // ----------------------------------------------------------------- misc ----
 // per song b: peak = max |wav[b]|; if peak > 1, wav[b] /= peak (n samples per song, n % 4 == 0)
-int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s);
+// decode guard (when guard != 0) then normalize_audio (when target_amp > 0), see small.hip
+int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s, float target_amp = 0.f,
+                       int guard = 1);
 int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s);
 
 }  // namespace acehip

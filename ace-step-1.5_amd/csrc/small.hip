@@ -150,14 +150,27 @@ __global__ __launch_bounds__(256) void wav_peak_kernel(const float4 *w, int64_t 
     }
 }
 
-__global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, const float *peak) {
+// One pass for the whole output path of a song:
+//  (1) the decode guard (generate_music_decode.py:193-195): divide by the peak when it
+//      exceeds 1 (IEEE division, as torch);
+//  (2) normalize_audio (audio_utils.py:24-62, inference.py:674-679) when target > 0:
+//      gain = fp32(target_amp) / peak', x *= gain, skipped when peak' < 1e-6.
+// peak' (the peak after (1)) needs no second reduction: division is monotone and
+// correctly rounded, so max|x / pk| = fl(pk / pk) = 1 exactly when (1) applied.
+__global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, const float *peak, int guard,
+                                                        float target) {
     const int b = blockIdx.y;
     const float pk = peak[b];
-    if (!(pk > 1.0f)) return;
+    const bool div = guard && pk > 1.0f;
+    const float p2 = div ? 1.0f : pk;
+    const bool norm = target > 0.f && !(p2 < 1e-6f);
+    if (!div && !norm) return;
+    const float gain = target / p2;
     float4 *p = w + (int64_t)b * n4;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
         float4 v = p[i];
-        v.x /= pk; v.y /= pk; v.z /= pk; v.w /= pk;
+        if (div) { v.x /= pk; v.y /= pk; v.z /= pk; v.w /= pk; }
+        if (norm) { v.x *= gain; v.y *= gain; v.z *= gain; v.w *= gain; }
         p[i] = v;
     }
 }
@@ -217,13 +230,13 @@ int fsq_codes_from_indices(const int *idx, int M, const FsqLevels &lv, bf16_t *c
     return 0;
 }
 
-int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s) {
+int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s, float target_amp, int guard) {
     HIP_TRY(hipMemsetAsync(peak, 0, (size_t)B * sizeof(float), s));
     const int64_t n4 = n / 4;
     const unsigned gx = (unsigned)std::min<int64_t>(1024, (n4 + 255) / 256);
     wav_peak_kernel<<<dim3(gx, B), 256, 0, s>>>((const float4 *)wav, n4, (unsigned *)peak);
     HIP_TRY(hipGetLastError());
-    wav_scale_kernel<<<dim3(gx, B), 256, 0, s>>>((float4 *)wav, n4, peak);
+    wav_scale_kernel<<<dim3(gx, B), 256, 0, s>>>((float4 *)wav, n4, peak, guard, target_amp);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -433,4 +433,13 @@ int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *s
     return wav_peak_normalize(wav, B, n, peak, (hipStream_t)stream);
 }
 
+// the guard above fused with normalize_audio(target_db) of acestep/inference.py:674-679
+// (audio_utils.py:24-62): one read pass (peak) + one read-write pass per song
+int acehip_wav_postprocess(float *wav, int B, int64_t n, float *peak, int guard, float target_amp, void *stream) {
+    if (!wav || !peak || B <= 0 || n <= 0) return fail(ACEHIP_E_ARG, "wav_postprocess: argument");
+    if (n % 4) return fail(ACEHIP_E_ARG, "wav_postprocess: samples per song must be a multiple of 4");
+    if (!(target_amp >= 0.f)) return fail(ACEHIP_E_ARG, "wav_postprocess: target_amp must be >= 0");
+    return wav_peak_normalize(wav, B, n, peak, (hipStream_t)stream, target_amp, guard);
+}
+
 }  // extern "C"

@@ -9,9 +9,14 @@ context [silence N(0,1) | ones]) followed by the full Oobleck VAE decode to
 48 kHz stereo.  One bench "step" = one song through the whole hot path
 (27 DiT forwards + 27 fused APG/Euler steps + VAE decode).
 
-Multi-GPU (``--gpus N`` under torchrun): one song per GPU per step (song-
-parallel), conditioning broadcast from rank 0 over RCCL, no
+Multi-GPU (``--gpus N``): one song per GPU per step (song-parallel, SURVEY
+§8e), one process per GPU.  Under a launcher (torchrun sets WORLD_SIZE) the
+ranks come from the environment and must equal N; started plainly with N > 1,
+bench.py spawns the N ranks itself (``acehip.distributed.launch_local``, before
+anything touches the GPU).  Conditioning is broadcast from rank 0 over RCCL, no
 collective inside the timed work; value = max-over-ranks time ÷ all songs.
+``--dry-run`` runs the same harness on CPU ranks over gloo with a stand-in song
+(the multi-rank CPU test drives it).
 
 Prints ONE JSON line on rank 0.  ``roofline`` is the dominant kernel (the
 SwiGLU gate/up GEMM, 2·M·N·K algorithmic FLOPs per launch) timed with HIP
@@ -63,14 +68,47 @@ def parse():
     p.add_argument("--repaint-end", type=float, default=120.0)
     p.add_argument("--text-len", type=int, default=128)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU ranks over gloo with a stand-in song: exercises the launcher / timing / "
+                        "max-over-ranks / JSON path without a GPU")
+    p.add_argument("--no-config1", action="store_true",
+                   help="skip the CPU run of BASELINE config 1 (10 s turbo, 8 steps, fp32, in full)")
     return p.parse_args()
+
+
+def host_cpus():
+    """(threads to use, host CPU count, CPU model).  Threads = the CPUs this process
+    may actually run on: its affinity set, capped by the cgroup CPU quota
+    (cpu.max).  On the GPU box os.cpu_count() reports the whole host (256) while
+    the job's quota is 16 CPUs; 256 threads on a 16-CPU quota would oversubscribe
+    it and time the scheduler, not the math."""
+    n_host = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = n_host
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                n = min(n, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, n_host, model
 
 
 def cpu_baseline(W_gpu, cfg, vae_w, vcfg, T, lenc, Bc=2, n_steps=1):
     """Time the CPU oracle (PyTorch fp32) on a bounded sample and extrapolate."""
     from oracle import dit_oracle, vae_oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads, _, _ = host_cpus()
     torch.set_num_threads(threads)
     W = {k: v.detach().float().cpu() for k, v in W_gpu.items()}
     g = torch.Generator().manual_seed(0)
@@ -98,21 +136,96 @@ def cpu_baseline(W_gpu, cfg, vae_w, vcfg, T, lenc, Bc=2, n_steps=1):
     return {"dit_step_s": dit_s, "vae_window_s": vae_s, "threads": threads, "window": win}
 
 
+def cpu_config1(W_gpu, cfg, lenc):
+    """BASELINE config 1 run IN FULL on the host: DiT-only text2music, 10 s of audio
+    (T = 250), the turbo 8-step table (shift 3), fp32, the PyTorch-CPU oracle
+    (oracle/dit_oracle.py + oracle/sampler_oracle.py) on the bench's weights."""
+    from oracle import dit_oracle, sampler_oracle
+    threads, n_host, model = host_cpus()
+    torch.set_num_threads(threads)
+    W = {k: v.detach().float().cpu() for k, v in W_gpu.items()}
+    g = torch.Generator().manual_seed(1)
+    T = 250
+    enc = torch.randn(1, lenc, cfg.hidden_size, generator=g)
+    ctx = torch.cat([torch.randn(1, T, 64, generator=g), torch.ones(1, T, 64)], -1)
+    noise = torch.randn(1, T, 64, generator=g)
+    with torch.no_grad():
+        t0 = time.time()
+        kv = dit_oracle.cross_kv(W, cfg, enc)
+        x = sampler_oracle.generate_turbo(lambda xt, tv: dit_oracle.dit_forward(W, cfg, xt, tv, tv, enc, ctx,
+                                                                                kv_cache=kv), noise, shift=3.0)
+        sec = time.time() - t0
+    assert torch.isfinite(x).all()
+    return {"value": round(sec, 2), "unit": "s/song", "cores": threads, "kind": "port", "cpu_model": model,
+            "host_cpus": n_host,
+            "config": "BASELINE configs[0]: DiT-only text2music, 10 s audio (T=250), turbo 8 steps shift 3, fp32 CPU",
+            "sample": "the whole song in full (cross K/V once + 8 DiT forwards + turbo Euler/x0), not extrapolated"}
+
+
 QWEN3_VOCAB = 151669   # Qwen3-Embedding-0.6B vocabulary
+
+
+def dry_run(args, rank, world):
+    """The multi-rank harness on CPU (gloo): same launch, barrier, timing, max-over-
+    ranks and JSON as the GPU run, with a fixed stand-in song (a small fp32 matmul
+    chain) — for the CPU test that --gpus N really yields N ranks."""
+    from acehip import distributed as D
+    torch.set_num_threads(1)
+    D.init(backend="gloo")
+    g = torch.Generator().manual_seed(1234)
+    cond = torch.randn(64, 64, generator=g) if rank == 0 else torch.zeros(64, 64)
+    t0 = time.time()
+    D.broadcast_condition([cond])
+    bcast_ms = (time.time() - t0) * 1e3
+    ref = torch.randn(64, 64, generator=torch.Generator().manual_seed(1234))
+    assert torch.equal(cond, ref), "conditioning broadcast mismatch"
+
+    def song(seed):
+        x = torch.randn(128, 128, generator=torch.Generator().manual_seed(seed))
+        for _ in range(20):
+            x = torch.tanh(x @ x.t() / 128)
+        return x
+
+    for i in range(args.warmup):
+        song(10_000 + rank * 100 + i)
+    D.barrier()
+    t0 = time.time()
+    for i in range(args.steps):
+        song(rank * 1000 + i)
+    D.barrier()
+    elapsed_max = D.max_over_ranks(time.time() - t0)
+    bc_all = D.gather_floats([bcast_ms])
+    songs = args.steps * world
+    if rank == 0:
+        print(json.dumps({"metric": "seconds/song (dry run: CPU stand-in song)", "value": round(elapsed_max / songs, 6),
+                          "unit": "s/song", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed_max / args.steps * 1e3, 3), "higher_is_better": False,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (CPU dry run)",
+                          "dry_run": True, "config": {"workload": "dry run", "global_batch": songs,
+                                                      "parallelism": f"song-parallel x{world}"},
+                          "ranks": world, "broadcast_ms_per_rank": [round(v, 3) for v in bc_all]}), flush=True)
+    D.destroy()
 
 
 def main():
     args = parse()
     from acehip import distributed as D
+    if D.needs_launch(args.gpus):
+        # one process per GPU: spawn the ranks before anything touches the GPU
+        sys.exit(D.launch_local([os.path.abspath(__file__), *sys.argv[1:]], args.gpus))
+    rank, world, local = D.env_world()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_run:
+        return dry_run(args, rank, world)
     from acehip.config import DiTConfig, VAEConfig
     from acehip.dit import AceStepDiTBackend, DiTRuntime
     from acehip.vae import OobleckBackend
     from acehip.weights import (synth_condenc_weights, synth_dit_weights, synth_null_condition,
                                 synth_text_encoder_weights, synth_vae_weights)
     from acehip.condition import ConditionEncoder, HipPrepareCondition, TextEncoder
-    from acehip.flops import dit_flops_per_row, vae_decoder_flops
+    from acehip.flops import dit_flops_executed_cfg_song_step, dit_flops_per_row, vae_decoder_flops
 
-    rank, world, local = D.env_world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     D.init(device=dev)
@@ -153,14 +266,24 @@ def main():
         vae = OobleckBackend(vcfg, local, max_T=T, with_encoder=args.repaint)
         vae.load(vae_w)
 
-    # synthetic conditioning on rank 0, broadcast over RCCL
+    # synthetic conditioning on rank 0, broadcast over RCCL; the
+    # broadcasts are timed per rank (outside the timed song loop, like the reference's
+    # batch preparation)
+    bcast_ms = [0.0]
+
+    def broadcast(ts):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        D.broadcast_condition(ts)
+        torch.cuda.synchronize()
+        bcast_ms[0] += (time.time() - t0) * 1e3
     g = torch.Generator(device=dev).manual_seed(1234)
     src = torch.randn(1, T, 64, device=dev, generator=g).bfloat16()          # silence latents
     chunk = torch.ones(1, T, 64, device=dev).bfloat16()
     if args.no_condition:
         enc = torch.randn(1, args.lenc, cfg.hidden_size, device=dev, generator=g).bfloat16()
         ctx = torch.cat([src, chunk], dim=-1).contiguous()
-        D.broadcast_condition([enc, ctx])
+        broadcast([enc, ctx])
         cond_kw = dict(encoder_hidden_states=enc, context_latents=ctx)
     else:
         # text / lyric token ids and a 30 s timbre reference; the text encoder and the
@@ -168,7 +291,7 @@ def main():
         text_ids = torch.randint(0, QWEN3_VOCAB, (1, args.text_len), device=dev, generator=g)
         lyric_ids = torch.randint(0, QWEN3_VOCAB, (1, args.lyric_len), device=dev, generator=g)
         refer = torch.randn(1, 750, cfg.timbre_hidden_dim, device=dev, generator=g).bfloat16()
-        D.broadcast_condition([text_ids, lyric_ids, refer, src])
+        broadcast([text_ids, lyric_ids, refer, src])
         cond_kw = dict(text_attention_mask=torch.ones(1, args.text_len, device=dev, dtype=torch.long),
                        lyric_attention_mask=torch.ones(1, args.lyric_len, device=dev, dtype=torch.long),
                        refer_audio_acoustic_hidden_states_packed=refer,
@@ -186,7 +309,7 @@ def main():
         sw = sw + 0.05 * torch.randn(sw.shape, device=dev, generator=g)
         src_wav = (sw / sw.abs().amax() * 10 ** (-12 / 20)).bfloat16().contiguous()
         del sw, tt
-        D.broadcast_condition([src_wav])
+        broadcast([src_wav])
         # conditioning_masks.py:37-50: latent span [start·48000//1920, end·48000//1920)
         span = (int(args.repaint_start * 48000 // 1920), int(args.repaint_end * 48000 // 1920))
         span_mask = torch.zeros(1, T, 64, device=dev, dtype=torch.bfloat16)
@@ -216,7 +339,9 @@ def main():
         e1.record()
         if vae is not None:
             wav = vae.decode_tensor(res["target_latents"].transpose(1, 2))
-            vae.peak_normalize_(wav)          # decode output guard (generate_music_decode.py:190-192)
+            # decode output guard (generate_music_decode.py:193-195) + the product's default
+            # normalize_audio(-1 dBFS) (inference.py:674-679), fused in one HIP pass pair
+            vae.postprocess_(wav, normalization_db=-1.0)
         e2.record()
         return e0, e1, e2
 
@@ -245,7 +370,12 @@ def main():
 
     songs = args.steps * world
     sec_per_song = elapsed_max / songs
+    bcast_all = D.gather_floats([bcast_ms[0]], dev)
     dit_flops_song = args.infer_steps * Bc * dit_flops_per_row(cfg, S, args.lenc)
+    # what the HIP path executes: the CFG null rows' cross-attention block and the
+    # layer-0 dedup are skipped algebraically (acehip.flops)
+    dit_flops_exec = (args.infer_steps * dit_flops_executed_cfg_song_step(cfg, S, args.lenc) if Bc == 2
+                      else dit_flops_song)
     vae_flops_song = vae_decoder_flops(vcfg, T) if vae is not None else 0.0
     M = Bc * S
     n_sw, ms_sw = prof["gemm_swiglu"]
@@ -302,8 +432,15 @@ def main():
         "dit_ms_note": "generate_audio wall on the GPU stream: (repaint: VAE encode +) condition encoders (once) + CFG DiT steps",
         "dit_ms_per_step": round(dit_ms / args.infer_steps, 3),
         "vae_ms_per_song": round(vae_ms, 2),
-        "dit_tflops": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
-        "dit_mfma_frac": round(dit_flops_song / (dit_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "dit_tflops_effective": round(dit_flops_song / (dit_ms * 1e-3) / 1e12, 1),
+        "dit_mfma_frac_effective": round(dit_flops_song / (dit_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "dit_tflops_executed": round(dit_flops_exec / (dit_ms * 1e-3) / 1e12, 1),
+        "dit_mfma_frac_executed": round(dit_flops_exec / (dit_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "dit_flops_note": "effective = the reference's algorithmic DiT FLOPs (SURVEY §8d) / DiT time; executed = "
+                          "the FLOPs the HIP path runs (CFG null-row cross-attention block and layer-0 CFG dedup "
+                          "skipped algebraically, -8.5 % at 240 s) / DiT time; both include the condition encoders' "
+                          "time in the denominator",
+        "broadcast_ms_per_rank": [round(v, 3) for v in bcast_all],
         "vae_tflops": round(vae_flops_song / (vae_ms * 1e-3) / 1e12, 1) if vae is not None else None,
         "roofline": roofline,
         "kernels": kernels,
@@ -323,13 +460,17 @@ def main():
                   f"1 full-size {kind}DiT step (Bc={Bc}, S={S}) = {cb['dit_step_s']:.2f}s x {args.infer_steps} "
                   f"+ one {cb['window']}-frame VAE decode window = {cb['vae_window_s']:.2f}s x {n_win}; "
                   f"fp32 PyTorch-CPU oracle, extrapolated")
+        n_thr, n_host, model = host_cpus()
         out["cpu_baseline"] = {"value": round(sec, 2 if full else 1), "unit": "s/song", "cores": cb["threads"],
-                               "kind": "port", "sample": sample}
+                               "kind": "port", "sample": sample, "cpu_model": model, "host_cpus": n_host,
+                               "cores_note": f"threads = this job's CPU quota ({n_thr} of the host's {n_host} "
+                                             "CPUs; the cgroup cpu.max caps it, more threads would only "
+                                             "oversubscribe the quota)"}
+        if not args.no_config1:
+            out["cpu_baseline_config1"] = cpu_config1(W, cfg, args.lenc)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    D.destroy()
 
 
 if __name__ == "__main__":

@@ -269,6 +269,16 @@ int acehip_vae_destroy(acehip_vae *h);
  * scratch of B floats (receives the peaks). */
 int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *stream);
 
+/* The guard above (guard != 0) fused with the product's loudness step,
+ * normalize_audio (acestep/audio_utils.py:24-62, applied per song at
+ * acestep/inference.py:674-679 when enable_normalization and normalization_db
+ * <= 0): after the guard, gain = target_amp / peak (fp32 division), wav *= gain,
+ * skipped for songs whose peak < 1e-6.  target_amp = fp32(10^(normalization_db/20));
+ * 0 = no normalization.  Bit-identical to the reference steps it replaces; one
+ * peak pass + one scale pass. */
+int acehip_wav_postprocess(float *wav, int B, int64_t n, float *peak, int guard, float target_amp,
+                           void *stream);
+
 /* ------------------------------------------------------------ kernels ---- */
 /* Single-kernel entry points used by the parity tests and the profiler
  * (same code the runtimes above launch). */

@@ -110,3 +110,41 @@ def test_wav_peak_normalize(gpu_device):
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ref)
     be.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("db", [-1.0, -3.0, 0.0, None])
+def test_wav_postprocess_guard_plus_normalize(gpu_device, db):
+    """§8f row 4: decode guard + normalize_audio fused in one HIP pass pair, bit-exact
+    against the reference's two steps (oracle/audio_oracle.py restates them)."""
+    from acehip.vae import OobleckBackend
+    from acehip.config import VAEConfig
+    from oracle import audio_oracle
+    be = OobleckBackend(VAEConfig.tiny(), 0, max_T=8, with_encoder=False)
+    g = torch.Generator().manual_seed(5)
+    wav = torch.randn(5, 2, 3840 * 7, generator=g)
+    wav[0] *= 0.2            # peak < 1: only normalized
+    wav[1] *= 2.5            # peak > 1: guard, then normalized
+    wav[2, 1, 77] = -7.0     # negative extreme sets the peak
+    wav[3] *= 1e-8           # near-silence: normalize_audio returns it unchanged
+    wav[4] = 0.0             # silence
+    ref = audio_oracle.decode_guard(wav.clone())
+    if db is not None:
+        ref = torch.stack([audio_oracle.normalize_audio(ref[b], db) for b in range(ref.shape[0])])
+    out = be.postprocess_(wav.to(gpu_device).contiguous(), normalization_db=db)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
+    be.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale,db", [(3.0, -1.0), (0.3, -1.0), (1e-8, -1.0), (0.7, -6.0)])
+def test_hip_normalize_audio_matches_reference(gpu_device, scale, db):
+    """integration.hip_normalize_audio (normalize_audio for device tensors, no guard)."""
+    from acehip.integration import hip_normalize_audio
+    from oracle import audio_oracle
+    a = torch.randn(2, 48000, generator=torch.Generator().manual_seed(2)) * scale
+    ref = audio_oracle.normalize_audio(a, db)
+    out = hip_normalize_audio(a.to(gpu_device), db)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
