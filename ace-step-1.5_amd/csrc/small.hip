@@ -154,7 +154,9 @@ __global__ __launch_bounds__(256) void wav_peak_kernel(const float4 *w, int64_t 
 //  (1) the decode guard (generate_music_decode.py:193-195): divide by the peak when it
 //      exceeds 1 (IEEE division, as torch);
 //  (2) normalize_audio (audio_utils.py:24-62, inference.py:674-679) when target > 0:
-//      gain = fp32(target_amp) / peak', x *= gain, skipped when peak' < 1e-6.
+//      gain = target_amp / peak' — a python float over a 0-d tensor, which torch
+//      evaluates as reciprocal(peak') * target (Tensor.__rtruediv__) — then x *= gain,
+//      skipped when peak' < 1e-6.
 // peak' (the peak after (1)) needs no second reduction: division is monotone and
 // correctly rounded, so max|x / pk| = fl(pk / pk) = 1 exactly when (1) applied.
 __global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, const float *peak, int guard,
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, c
     const float p2 = div ? 1.0f : pk;
     const bool norm = target > 0.f && !(p2 < 1e-6f);
     if (!div && !norm) return;
-    const float gain = target / p2;
+    const float gain = (1.0f / p2) * target;
     float4 *p = w + (int64_t)b * n4;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
         float4 v = p[i];

@@ -272,7 +272,8 @@ int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *s
 /* The guard above (guard != 0) fused with the product's loudness step,
  * normalize_audio (acestep/audio_utils.py:24-62, applied per song at
  * acestep/inference.py:674-679 when enable_normalization and normalization_db
- * <= 0): after the guard, gain = target_amp / peak (fp32 division), wav *= gain,
+ * <= 0): after the guard, gain = (1 / peak) * target_amp (fp32, the order torch
+ * evaluates float / tensor in), wav *= gain,
  * skipped for songs whose peak < 1e-6.  target_amp = fp32(10^(normalization_db/20));
  * 0 = no normalization.  Bit-identical to the reference steps it replaces; one
  * peak pass + one scale pass. */

@@ -107,9 +107,9 @@ class LoraLinear(torch.nn.Module):
         out_f, in_f = base.weight.shape
         g = torch.Generator().manual_seed(seed)
         self.lora_A = torch.nn.ParameterDict({"default": torch.nn.Parameter(
-            (torch.randn(r, in_f, generator=g) * 0.1).to(dev, torch.bfloat16), requires_grad=False)})
+            (torch.randn(r, in_f, generator=g) * 0.3).to(dev, torch.bfloat16), requires_grad=False)})
         self.lora_B = torch.nn.ParameterDict({"default": torch.nn.Parameter(
-            (torch.randn(out_f, r, generator=g) * 0.1).to(dev, torch.bfloat16), requires_grad=False)})
+            (torch.randn(out_f, r, generator=g) * 0.3).to(dev, torch.bfloat16), requires_grad=False)})
         self.scaling = {"default": scale}
         self.active_adapters = ["default"]
         self.merged = False
@@ -314,6 +314,7 @@ def test_install_lora_repack_vs_oracle(gpu_device, installed):
             return dit_oracle.dit_forward(Wb, cfg, xt, tb, tb, enc, ctx).float()
 
     base = hip()
+    ref_base = oracle(h.model.W)
     for scale in (1.0, 0.35):
         if scale == 1.0:
             h.add_lora("synthetic", scale=1.0)                   # wrapped by install -> re-pack
@@ -329,6 +330,9 @@ def test_install_lora_repack_vs_oracle(gpu_device, installed):
             W[name + ".weight"] = (lo.base_layer.weight.float() + lo.get_delta_weight("default")).bfloat16()
         got, ref = hip(), oracle(W)
         assert rel_l2(got, ref) <= 0.025 and cosine(got, ref) >= 0.999, (scale, rel_l2(got, ref))
-        assert rel_l2(got, base) > 0.02                           # the adapters matter
+        # the adapters' effect (through gated residuals it is ~1 % of the output here) is
+        # tracked: HIP's change equals the oracle's change
+        assert rel_l2(got, base) > 0.004
+        assert rel_l2(got - base, ref - ref_base) < 0.15, rel_l2(got - base, ref - ref_base)
     h.unload_lora()
     assert torch.equal(hip(), base)
