@@ -38,7 +38,7 @@ class DiTCfg(ctypes.Structure):
                 ("head_dim", c_int), ("layers", c_int), ("window", c_int), ("patch", c_int),
                 ("in_channels", c_int), ("out_channels", c_int), ("eps", c_float),
                 ("rope_theta", c_float), ("max_S", c_int), ("max_Bc", c_int), ("max_Lenc", c_int),
-                ("sliding", POINTER(c_uint8))]
+                ("sliding", POINTER(c_uint8)), ("fp32", c_int)]
 
 
 class EncCfg(ctypes.Structure):
@@ -68,7 +68,7 @@ def _declare(lib):
         "acehip_dit_finalize": (c_int, [P]),
         "acehip_dit_set_condition": (c_int, [P, P, c_int, c_int, P]),
         "acehip_dit_set_uniform_rows": (c_int, [P, c_int, P]),
-        "acehip_dit_forward": (c_int, [P, P, P, c_int, P, P, c_int, c_int, c_int, P, P]),
+        "acehip_dit_forward": (c_int, [P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, P, P]),
         "acehip_dit_destroy": (c_int, [P]),
         "acehip_dit_set_graph": (c_int, [P, c_int]),
         "acehip_dit_profile": (c_int, [P, c_int]),

@@ -48,8 +48,13 @@ class DiTRuntime:
     """One ``acehip_dit`` handle: packed weights, cross-K/V cache, workspace."""
 
     def __init__(self, cfg: DiTConfig, device: Union[int, torch.device] = 0, max_S: int = 7500,
-                 max_Bc: int = 2, max_Lenc: int = 1024):
+                 max_Bc: int = 2, max_Lenc: int = 1024, dtype: torch.dtype = torch.bfloat16):
+        """dtype bfloat16: the production path; float32: the fp32 parity mode (SURVEY
+        §8c(iii) — the reference's fp32 forward, fp32 weights / activations / accumulation)."""
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("DiTRuntime: dtype must be torch.bfloat16 or torch.float32")
         self.cfg = cfg
+        self.dtype = dtype
         self.device = torch.device("cuda", device if isinstance(device, int) else device.index or 0)
         self.max_S, self.max_Bc, self.max_Lenc = max_S, max_Bc, max_Lenc
         sl = (_ffi.c_uint8 * cfg.num_hidden_layers)(
@@ -62,7 +67,8 @@ class DiTRuntime:
                         in_channels=cfg.in_channels, out_channels=cfg.audio_acoustic_hidden_dim,
                         eps=cfg.rms_norm_eps, rope_theta=cfg.rope_theta, max_S=max_S,
                         max_Bc=max_Bc, max_Lenc=max_Lenc,
-                        sliding=_ffi.ctypes.cast(sl, _ffi.POINTER(_ffi.c_uint8)))
+                        sliding=_ffi.ctypes.cast(sl, _ffi.POINTER(_ffi.c_uint8)),
+                        fp32=1 if dtype == torch.float32 else 0)
         h = _ffi.c_void_p()
         check(lib().acehip_dit_create(self.device.index, _ffi.ctypes.byref(c), _ffi.ctypes.byref(h)),
               "dit_create")
@@ -99,8 +105,8 @@ class DiTRuntime:
 
     # -- compute -------------------------------------------------------------
     def set_condition(self, enc: torch.Tensor):
-        """enc: [Bc, Lenc, D] bf16 on the device (pre condition_embedder)."""
-        enc = enc.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        """enc: [Bc, Lenc, D] on the device (pre condition_embedder), cast to the runtime dtype."""
+        enc = enc.to(device=self.device, dtype=self.dtype).contiguous()
         Bc, Lenc, _ = enc.shape
         check(lib().acehip_dit_set_condition(self.h, ptr(enc), Bc, Lenc, stream_ptr()), "set_condition")
         self._enc_keepalive = enc
@@ -113,19 +119,21 @@ class DiTRuntime:
 
     def forward(self, xt: torch.Tensor, ctx: torch.Tensor, t: torch.Tensor,
                 t_r: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One decoder forward.  xt [Bx,T,64], ctx [Bx,T,128] bf16; t/t_r: fp32
-        device tensors of 1 (broadcast) or Bc elements.  Returns vt [Bc,T,64]."""
+        """One decoder forward.  xt [Bx,T,64], ctx [Bx,T,128] in the runtime dtype; t/t_r:
+        fp32 device tensors of 1 (broadcast) or Bc elements.  Returns vt [Bc,T,64]."""
         Bx, T, _ = xt.shape
         Bc = self.Bc
         assert Bc is not None, "set_condition first"
-        assert xt.dtype == torch.bfloat16 and ctx.dtype == torch.bfloat16
+        assert xt.dtype == self.dtype and ctx.dtype == self.dtype, (xt.dtype, ctx.dtype, self.dtype)
         assert xt.is_contiguous() and ctx.is_contiguous() and ctx.shape[:2] == xt.shape[:2]
         if t_r is None:
             t_r = t
         stride = 0 if t.numel() == 1 else 1
         if out is None:
-            out = torch.empty(Bc, T, 64, device=xt.device, dtype=torch.bfloat16)
-        check(lib().acehip_dit_forward(self.h, ptr(xt), ptr(ctx), Bx, ptr(t), ptr(t_r), stride, Bc, T,
+            out = torch.empty(Bc, T, 64, device=xt.device, dtype=self.dtype)
+        assert out.dtype == self.dtype and out.is_contiguous()
+        dt = ACEHIP_F32 if self.dtype == torch.float32 else ACEHIP_BF16
+        check(lib().acehip_dit_forward(self.h, ptr(xt), ptr(ctx), Bx, ptr(t), ptr(t_r), stride, Bc, T, dt,
                                        ptr(out), stream_ptr()), "dit_forward")
         return out
 

@@ -26,7 +26,9 @@ using namespace acehip;
 
 namespace {
 
-enum PackKind { P_COPY, P_GU_GATE, P_GU_UP, P_PROJ_IN, P_PROJ_OUT_W, P_PROJ_OUT_B, P_F32 };
+enum PackKind { P_COPY, P_GU_GATE, P_GU_UP, P_PROJ_IN, P_PROJ_OUT_W, P_PROJ_OUT_B,
+                // fp32 parity mode: fp32 destinations, reference layouts except the patch convs
+                P_F32, P_F32_PROJ_IN, P_F32_PROJ_OUT_W, P_F32_PROJ_OUT_B };
 
 struct Slot {
     bf16_t *dst = nullptr;
@@ -91,9 +93,31 @@ struct acehip_dit {
     hipStream_t cap_stream = nullptr;
     hipGraphExec_t gexec = nullptr;
     int gkey[5] = {-1, -1, -1, -1, -1};
+
+    // fp32 parity mode (acehip_dit_cfg.fp32): fp32 weights and workspace,
+    // the kernels of f32.hip; the bf16 buffers above are not allocated
+    bool f32 = false;
+    struct F32 {
+        struct Layer {
+            float *n_sa, *n_ca, *n_mlp, *wqkv, *wo, *qn, *kn, *cqn, *ckn, *wcq, *wckv, *wco, *wg, *wu, *wdown;
+        };
+        std::vector<Layer> layers;
+        float *tables, *sst_out, *win, *bin, *wce, *bce, *norm_out, *wout, *bout;
+        float *te_l1[2], *te_b1[2], *te_l2[2], *te_b2[2], *te_tp[2], *te_btp[2];
+        float *rope_cos, *rope_sin;
+        float *X, *XN, *QKV, *Qh, *Kh, *Vh, *AO, *G, *U, *Hb, *Xin, *O2;
+        float *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
+        float *Kc, *Vc, *E, *KVtmp;
+    } f{};
 };
 
 static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s);
+static int create_f32(acehip_dit *h);
+static int set_weight_f32(acehip_dit *h, Slot &s, const void *ptr, int dtype, int64_t n, int on_device);
+static int build_rope_f32(acehip_dit *h);
+static int set_condition_f32(acehip_dit *h, const float *enc, int Bc, int Lenc, hipStream_t s);
+static int forward_f32(acehip_dit *h, const float *xt, const float *ctx, int Bx, const float *t, const float *t_r,
+                       int t_stride, int Bc, int T, float *vt_out, hipStream_t s);
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
 static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
@@ -199,6 +223,18 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->cfg.sliding = nullptr;
     const char *ge = getenv("ACEHIP_DIT_GRAPH");
     h->graph_on = ge && ge[0] == '1';
+    if (cfg->fp32) {
+        h->f32 = true;
+        h->graph_on = false;
+        const int rc = create_f32(h);
+        if (rc) {
+            const std::string e = acehip_last_error();
+            acehip_dit_destroy(h);
+            return fail(rc, e);
+        }
+        *out = h;
+        return 0;
+    }
     const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L;
     bool ok = true;
     auto A = [&](size_t n) { bf16_t *p = dalloc(h, n); ok = ok && p; return p; };
@@ -337,6 +373,7 @@ int acehip_dit_set_weight(acehip_dit *h, const char *name, const void *ptr, int 
     }
     const int64_t n = numel(sh);
     if (dtype != ACEHIP_F32 && dtype != ACEHIP_BF16) return fail(ACEHIP_E_ARG, "dtype");
+    if (h->f32) return set_weight_f32(h, s, ptr, dtype, n, on_device);
     // bring to a contiguous bf16 device source
     const bf16_t *src = nullptr;
     std::vector<bf16_t> hb;
@@ -422,7 +459,7 @@ int acehip_dit_finalize(acehip_dit *h) {
         if (!kv.second.set) missing += kv.first + " ";
     if (!missing.empty()) return fail(ACEHIP_E_STATE, "dit_finalize: missing weights: " + missing.substr(0, 400));
     if (h->F % 32) return fail(ACEHIP_E_ARG, "intermediate must be a multiple of 32");
-    int rc = build_rope(h);
+    int rc = h->f32 ? build_rope_f32(h) : build_rope(h);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
     h->finalized = true;
@@ -436,6 +473,7 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
         return fail(ACEHIP_E_ARG, "set_condition: Bc/Lenc out of range");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    if (h->f32) return set_condition_f32(h, (const float *)enc, Bc, Lenc, s);
     const int D = h->D, kvd = h->kvd, M = Bc * Lenc;
     GemmArgs g{};
     g.A = (const bf16_t *)enc; g.lda = D; g.W = h->wce; g.ldw = D; g.C = h->E; g.ldc = D;
@@ -470,6 +508,7 @@ int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     h->uniform_from = 1 << 30;
     if (first_row == h->cond_Bc) return 0;   // none uniform
+    if (h->f32) return 0;                    // parity mode: every row computed in full
     const int D = h->D, qd = h->qd, kvd = h->kvd, Le = h->cond_Lenc;
     const size_t per = (size_t)h->cond_Bc * kvd * Le;
     for (int l = 0; l < h->L; ++l) {
@@ -488,14 +527,20 @@ int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream) {
 }
 
 int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, const float *t,
-                       const float *t_r, int t_stride, int Bc, int T, void *vt_out, void *stream) {
+                       const float *t_r, int t_stride, int Bc, int T, int dtype, void *vt_out, void *stream) {
     if (!h || !xt || !ctx || !t || !t_r || !vt_out) return fail(ACEHIP_E_ARG, "null argument");
     if (!h->finalized || !h->have_cond) return fail(ACEHIP_E_STATE, "forward before finalize/set_condition");
     if (Bc != h->cond_Bc) return fail(ACEHIP_E_ARG, "forward: Bc differs from set_condition");
+    if (dtype != (h->f32 ? ACEHIP_F32 : ACEHIP_BF16))
+        return fail(ACEHIP_E_ARG, h->f32 ? "forward: this handle is the fp32 parity mode (dtype ACEHIP_F32)"
+                                         : "forward: this handle is bf16 (dtype ACEHIP_BF16); create with fp32=1 "
+                                           "for the fp32 parity mode");
     const int S = (T + 1) / 2;
     if (T <= 0 || S > h->cfg.max_S || Bx <= 0 || Bc % Bx) return fail(ACEHIP_E_ARG, "forward: T/Bx out of range");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    if (h->f32)
+        return forward_f32(h, (const float *)xt, (const float *)ctx, Bx, t, t_r, t_stride, Bc, T, (float *)vt_out, s);
     const int M = Bc * S;
     int rc;
 #define RUN(x) do { if ((rc = (x))) return rc; } while (0)
@@ -540,7 +585,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
 
 int acehip_dit_set_graph(acehip_dit *h, int enable) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
-    h->graph_on = enable != 0;
+    h->graph_on = enable != 0 && !h->f32;
     return 0;
 }
 
@@ -804,3 +849,266 @@ int acehip_attention_masked_bf16(const void *q, const void *k, const void *v, vo
 }
 
 }  // extern "C"
+
+// ===================================================================== fp32 ====
+// The fp32 parity mode (acehip_dit_cfg.fp32 = 1): the reference's
+// fp32 forward (what it runs on a non-cuda device, init_service_orchestrator.py:51)
+// with fp32 weights and activations throughout, on the kernels of f32.hip.  No
+// algebraic shortcuts (no CFG-row dedup, no closed-form null rows, no graphs).
+
+static float *falloc(acehip_dit *h, size_t elems) {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(elems, 1) * 4) != hipSuccess) return nullptr;
+    h->allocs.push_back(p);
+    return (float *)p;
+}
+
+static void add_slot_f32(acehip_dit *h, const std::string &name, float *dst, std::vector<int64_t> shape,
+                         PackKind kind = P_F32) {
+    Slot s;
+    s.dst_f32 = dst;
+    s.shape = std::move(shape);
+    s.kind = kind;
+    h->slots[name] = s;
+}
+
+static int create_f32(acehip_dit *h) {
+    const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L;
+    bool ok = true;
+    auto A = [&](size_t n) { float *p = falloc(h, n); ok = ok && p; return p; };
+    auto &f = h->f;
+    f.tables = A((size_t)L * 6 * D);
+    f.layers.resize(L);
+    for (int i = 0; i < L && ok; ++i) {
+        auto &ly = f.layers[i];
+        ly.n_sa = A(D); ly.n_ca = A(D); ly.n_mlp = A(D);
+        ly.wqkv = A((size_t)(qd + 2 * kvd) * D); ly.wo = A((size_t)D * qd);
+        ly.qn = A(128); ly.kn = A(128); ly.cqn = A(128); ly.ckn = A(128);
+        ly.wcq = A((size_t)qd * D); ly.wckv = A((size_t)2 * kvd * D); ly.wco = A((size_t)D * qd);
+        ly.wg = A((size_t)F * D); ly.wu = A((size_t)F * D); ly.wdown = A((size_t)D * F);
+        if (!ok) break;
+        const std::string p = "layers." + std::to_string(i);
+        add_slot_f32(h, p + ".scale_shift_table", f.tables + (size_t)i * 6 * D, {1, 6, D});
+        add_slot_f32(h, p + ".self_attn_norm.weight", ly.n_sa, {D});
+        add_slot_f32(h, p + ".cross_attn_norm.weight", ly.n_ca, {D});
+        add_slot_f32(h, p + ".mlp_norm.weight", ly.n_mlp, {D});
+        add_slot_f32(h, p + ".self_attn.q_proj.weight", ly.wqkv, {qd, D});
+        add_slot_f32(h, p + ".self_attn.k_proj.weight", ly.wqkv + (size_t)qd * D, {kvd, D});
+        add_slot_f32(h, p + ".self_attn.v_proj.weight", ly.wqkv + (size_t)(qd + kvd) * D, {kvd, D});
+        add_slot_f32(h, p + ".self_attn.o_proj.weight", ly.wo, {D, qd});
+        add_slot_f32(h, p + ".self_attn.q_norm.weight", ly.qn, {128});
+        add_slot_f32(h, p + ".self_attn.k_norm.weight", ly.kn, {128});
+        add_slot_f32(h, p + ".cross_attn.q_proj.weight", ly.wcq, {qd, D});
+        add_slot_f32(h, p + ".cross_attn.k_proj.weight", ly.wckv, {kvd, D});
+        add_slot_f32(h, p + ".cross_attn.v_proj.weight", ly.wckv + (size_t)kvd * D, {kvd, D});
+        add_slot_f32(h, p + ".cross_attn.o_proj.weight", ly.wco, {D, qd});
+        add_slot_f32(h, p + ".cross_attn.q_norm.weight", ly.cqn, {128});
+        add_slot_f32(h, p + ".cross_attn.k_norm.weight", ly.ckn, {128});
+        add_slot_f32(h, p + ".mlp.gate_proj.weight", ly.wg, {F, D});
+        add_slot_f32(h, p + ".mlp.up_proj.weight", ly.wu, {F, D});
+        add_slot_f32(h, p + ".mlp.down_proj.weight", ly.wdown, {D, F});
+    }
+    f.sst_out = A(2 * D); f.win = A((size_t)D * 384); f.bin = A(D);
+    f.wce = A((size_t)D * D); f.bce = A(D); f.norm_out = A(D);
+    f.wout = A((size_t)128 * D); f.bout = A(128);
+    const char *te_names[2] = {"time_embed", "time_embed_r"};
+    for (int e = 0; e < 2 && ok; ++e) {
+        f.te_l1[e] = A((size_t)D * 256); f.te_b1[e] = A(D);
+        f.te_l2[e] = A((size_t)D * D); f.te_b2[e] = A(D);
+        f.te_tp[e] = A((size_t)6 * D * D); f.te_btp[e] = A(6 * D);
+        if (!ok) break;
+        const std::string p = te_names[e];
+        add_slot_f32(h, p + ".linear_1.weight", f.te_l1[e], {D, 256});
+        add_slot_f32(h, p + ".linear_1.bias", f.te_b1[e], {D});
+        add_slot_f32(h, p + ".linear_2.weight", f.te_l2[e], {D, D});
+        add_slot_f32(h, p + ".linear_2.bias", f.te_b2[e], {D});
+        add_slot_f32(h, p + ".time_proj.weight", f.te_tp[e], {6 * D, D});
+        add_slot_f32(h, p + ".time_proj.bias", f.te_btp[e], {6 * D});
+    }
+    if (ok) {
+        add_slot_f32(h, "scale_shift_table", f.sst_out, {1, 2, D});
+        add_slot_f32(h, "proj_in.1.weight", f.win, {D, 192, 2}, P_F32_PROJ_IN);
+        add_slot_f32(h, "proj_in.1.bias", f.bin, {D});
+        add_slot_f32(h, "condition_embedder.weight", f.wce, {D, D});
+        add_slot_f32(h, "condition_embedder.bias", f.bce, {D});
+        add_slot_f32(h, "norm_out.weight", f.norm_out, {D});
+        add_slot_f32(h, "proj_out.1.weight", f.wout, {D, 64, 2}, P_F32_PROJ_OUT_W);
+        add_slot_f32(h, "proj_out.1.bias", f.bout, {64}, P_F32_PROJ_OUT_B);
+    }
+    const size_t S = h->cfg.max_S, Bc = h->cfg.max_Bc, M = S * Bc, Le = h->cfg.max_Lenc;
+    f.X = A(M * D); f.XN = A(M * D); f.QKV = A(M * (qd + 2 * kvd));
+    f.Qh = A(M * qd); f.Kh = A(M * kvd); f.Vh = A(M * kvd); f.AO = A(M * qd);
+    f.G = A(M * F); f.U = A(M * F); f.Hb = A(M * F); f.Xin = A(M * 384); f.O2 = A(M * 128);
+    for (int e = 0; e < 2; ++e) { f.emb[e] = A(Bc * 256); f.temb_e[e] = A(Bc * D); f.proj_e[e] = A(Bc * 6 * D); }
+    f.h1 = A(Bc * D); f.temb = A(Bc * D); f.proj = A(Bc * 6 * D);
+    f.mod = A((size_t)L * Bc * 6 * D); f.mod_out = A(Bc * 2 * D);
+    f.Kc = A((size_t)L * Bc * kvd * Le); f.Vc = A((size_t)L * Bc * kvd * Le);
+    f.E = A(Bc * Le * D); f.KVtmp = A(Bc * Le * 2 * kvd);
+    f.rope_cos = A(S * 128); f.rope_sin = A(S * 128);
+    h->freqs = A(128);
+    if (!ok) return fail(ACEHIP_E_OOM, "dit_create (fp32): device allocation failed");
+    float fr[128];
+    for (int i = 0; i < 128; ++i) fr[i] = expf((-9.210340371976184f * (float)i) / 128.0f);
+    HIP_TRY(hipMemcpy(h->freqs, fr, sizeof(fr), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// every fp32 weight goes through the host (parity mode: load time is not a concern)
+static int set_weight_f32(acehip_dit *h, Slot &s, const void *ptr, int dtype, int64_t n, int on_device) {
+    std::vector<float> v(n);
+    if (dtype == ACEHIP_F32) {
+        HIP_TRY(hipMemcpy(v.data(), ptr, n * 4, on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+    } else {
+        std::vector<bf16_t> b(n);
+        HIP_TRY(hipMemcpy(b.data(), ptr, n * 2, on_device ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+        for (int64_t i = 0; i < n; ++i) v[i] = bf2f(b[i]);
+    }
+    std::vector<float> out;
+    const std::vector<float> *src = &v;
+    if (s.kind == P_F32_PROJ_IN) {            // [D][192][2] → [D][k·192 + c]
+        const int64_t D = s.shape[0];
+        out.resize(n);
+        for (int64_t o = 0; o < D; ++o)
+            for (int c = 0; c < 192; ++c)
+                for (int k = 0; k < 2; ++k) out[o * 384 + k * 192 + c] = v[(o * 192 + c) * 2 + k];
+        src = &out;
+    } else if (s.kind == P_F32_PROJ_OUT_W) {  // [D][64][2] → [k·64 + o][D]
+        const int64_t D = s.shape[0];
+        out.resize(n);
+        for (int64_t c = 0; c < D; ++c)
+            for (int o = 0; o < 64; ++o)
+                for (int k = 0; k < 2; ++k) out[(k * 64 + o) * D + c] = v[(c * 64 + o) * 2 + k];
+        src = &out;
+    } else if (s.kind == P_F32_PROJ_OUT_B) {  // [64] → [k·64 + o]
+        out.resize(128);
+        for (int k = 0; k < 2; ++k)
+            for (int o = 0; o < 64; ++o) out[k * 64 + o] = v[o];
+        src = &out;
+    } else if (s.kind != P_F32) {
+        return fail(ACEHIP_E_ARG, "dit_set_weight (fp32): unexpected slot");
+    }
+    HIP_TRY(hipMemcpy(s.dst_f32, src->data(), src->size() * 4, hipMemcpyHostToDevice));
+    s.set = true;
+    return 0;
+}
+
+// Qwen3RotaryEmbedding in fp32: inv_freq stays fp32 (no .to(bf16) in an fp32 model),
+// angle = fp32(pos · inv_freq), cos/sin of it
+static int build_rope_f32(acehip_dit *h) {
+    const int hd = h->cfg.head_dim, S = h->cfg.max_S;
+    std::vector<float> inv(hd / 2);
+    for (int i = 0; i < hd / 2; ++i)
+        inv[i] = !h->inv_freq_override.empty() ? h->inv_freq_override[i]
+                                               : 1.0f / powf(h->cfg.rope_theta, (float)(2 * i) / (float)hd);
+    std::vector<float> c((size_t)S * hd), sn((size_t)S * hd);
+    for (int p = 0; p < S; ++p)
+        for (int i = 0; i < hd; ++i) {
+            const float a = (float)p * inv[i % (hd / 2)];
+            c[(size_t)p * hd + i] = (float)cos((double)a);
+            sn[(size_t)p * hd + i] = (float)sin((double)a);
+        }
+    HIP_TRY(hipMemcpy(h->f.rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->f.rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int set_condition_f32(acehip_dit *h, const float *enc, int Bc, int Lenc, hipStream_t s) {
+    auto &f = h->f;
+    const int D = h->D, kvd = h->kvd, M = Bc * Lenc;
+    int rc;
+    GemmF32Args g{};
+    g.A = enc; g.lda = D; g.W = f.wce; g.ldw = D; g.C = f.E; g.ldc = D; g.M = M; g.N = D; g.K = D;
+    g.epi = EPI_STORE; g.bias = f.bce;
+    if ((rc = gemm_f32(g, s))) return rc;
+    const size_t per = (size_t)Bc * kvd * Lenc;
+    for (int l = 0; l < h->L; ++l) {
+        GemmF32Args k{};
+        k.A = f.E; k.lda = D; k.W = f.layers[l].wckv; k.ldw = D; k.C = f.KVtmp; k.ldc = 2 * kvd;
+        k.M = M; k.N = 2 * kvd; k.K = D; k.epi = EPI_STORE;
+        if ((rc = gemm_f32(k, s))) return rc;
+        HeadPostF32Args p{};
+        p.src = f.KVtmp; p.ld_src = 2 * kvd; p.B = Bc; p.S = Lenc; p.nq = 0;
+        p.nk = h->cfg.kv_heads; p.nv = h->cfg.kv_heads; p.kw = f.layers[l].ckn;
+        p.k = f.Kc + l * per; p.v = f.Vc + l * per; p.S_dst = Lenc; p.eps = h->cfg.eps;
+        if ((rc = head_post_f32(p, s))) return rc;
+    }
+    h->have_cond = true;
+    h->cond_Bc = Bc;
+    h->cond_Lenc = Lenc;
+    h->uniform_from = 1 << 30;
+    return 0;
+}
+
+static int forward_f32(acehip_dit *h, const float *xt, const float *ctx, int Bx, const float *t, const float *t_r,
+                       int t_stride, int Bc, int T, float *vt_out, hipStream_t s) {
+    auto &f = h->f;
+    const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L, S = (T + 1) / 2, M = Bc * S;
+    const int H = h->cfg.heads, KV = h->cfg.kv_heads, Le = h->cond_Lenc;
+    const float eps = h->cfg.eps, scale = 1.0f / sqrtf((float)h->cfg.head_dim);
+    const int64_t mbs = 6 * D;
+    const size_t cper = (size_t)Bc * kvd * Le;
+    int rc;
+#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
+    auto gemm = [&](const float *A, int lda, const float *W, float *C, int ldc, int m, int n, int k, const float *bias,
+                    int epi, const float *gate = nullptr) {
+        GemmF32Args g{};
+        g.A = A; g.lda = lda; g.W = W; g.ldw = k; g.C = C; g.ldc = ldc; g.M = m; g.N = n; g.K = k; g.bias = bias;
+        g.epi = epi; g.res = C; g.ldr = ldc; g.gate = gate; g.gate_bstride = mbs; g.rows_per_batch = S;
+        return gemm_f32(g, s);
+    };
+    // timestep embeddings (base:225-254, :1340-1344)
+    for (int e = 0; e < 2; ++e) {
+        RUN(timestep_sinusoid_f32(t, t_r, t_stride, e, Bc, h->freqs, f.emb[e], s));
+        RUN(gemv_f32(f.emb[e], 256, f.te_l1[e], f.te_b1[e], f.h1, D, Bc, D, 256, 0, s));
+        RUN(gemv_f32(f.h1, D, f.te_l2[e], f.te_b2[e], f.temb_e[e], D, Bc, D, D, 1, s));
+        RUN(gemv_f32(f.temb_e[e], D, f.te_tp[e], f.te_btp[e], f.proj_e[e], 6 * D, Bc, 6 * D, D, 1, s));
+    }
+    RUN(add_f32(f.temb_e[0], f.temb_e[1], f.temb, (int64_t)Bc * D, s));
+    RUN(add_f32(f.proj_e[0], f.proj_e[1], f.proj, (int64_t)Bc * 6 * D, s));
+    RUN(modulation_f32(f.tables, L, 6, f.proj, Bc, D, f.mod, s));
+    RUN(modulation_f32(f.sst_out, 1, 2, f.temb, Bc, D, f.mod_out, s));
+    // concat + pad + proj_in (base:1347-1358)
+    RUN(pack_patches_f32(xt, ctx, Bx, Bc, T, S, f.Xin, s));
+    RUN(gemm(f.Xin, 384, f.win, f.X, D, M, D, 384, f.bin, EPI_STORE));
+    for (int l = 0; l < L; ++l) {
+        const auto &ly = f.layers[l];
+        const float *md = f.mod + (size_t)l * Bc * 6 * D;
+        // self-attention, AdaLN-Zero (base:499-511)
+        RUN(rmsnorm_f32(f.X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, f.XN, M, D, eps, s));
+        RUN(gemm(f.XN, D, ly.wqkv, f.QKV, qd + 2 * kvd, M, qd + 2 * kvd, D, nullptr, EPI_STORE));
+        HeadPostF32Args p{};
+        p.src = f.QKV; p.ld_src = qd + 2 * kvd; p.B = Bc; p.S = S; p.nq = H; p.nk = KV; p.nv = KV;
+        p.qw = ly.qn; p.kw = ly.kn; p.cos = f.rope_cos; p.sin = f.rope_sin;
+        p.q = f.Qh; p.k = f.Kh; p.v = f.Vh; p.S_dst = S; p.eps = eps;
+        RUN(head_post_f32(p, s));
+        AttnF32Args at{};
+        at.q = f.Qh; at.k = f.Kh; at.v = f.Vh; at.o = f.AO; at.o_ld = qd; at.B = Bc; at.H = H; at.KV = KV;
+        at.Sq = S; at.Sk = S; at.window = h->sliding[l] ? h->cfg.window : -1; at.scale = scale;
+        RUN(attention_f32(at, s));
+        RUN(gemm(f.AO, qd, ly.wo, f.X, D, M, D, qd, nullptr, EPI_GATED_RES, md + 2 * D));
+        // cross-attention, plain residual (base:513-526)
+        RUN(rmsnorm_f32(f.X, ly.n_ca, nullptr, nullptr, 0, S, f.XN, M, D, eps, s));
+        RUN(gemm(f.XN, D, ly.wcq, f.QKV, qd, M, qd, D, nullptr, EPI_STORE));
+        HeadPostF32Args cq{};
+        cq.src = f.QKV; cq.ld_src = qd; cq.B = Bc; cq.S = S; cq.nq = H; cq.qw = ly.cqn; cq.q = f.Qh;
+        cq.S_dst = S; cq.eps = eps;
+        RUN(head_post_f32(cq, s));
+        AttnF32Args ca{};
+        ca.q = f.Qh; ca.k = f.Kc + l * cper; ca.v = f.Vc + l * cper; ca.o = f.AO; ca.o_ld = qd; ca.B = Bc;
+        ca.H = H; ca.KV = KV; ca.Sq = S; ca.Sk = Le; ca.window = -1; ca.scale = scale;
+        RUN(attention_f32(ca, s));
+        RUN(gemm(f.AO, qd, ly.wco, f.X, D, M, D, qd, nullptr, EPI_RES));
+        // SwiGLU MLP, AdaLN-Zero (base:528-533)
+        RUN(rmsnorm_f32(f.X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, f.XN, M, D, eps, s));
+        RUN(gemm(f.XN, D, ly.wg, f.G, F, M, F, D, nullptr, EPI_STORE));
+        RUN(gemm(f.XN, D, ly.wu, f.U, F, M, F, D, nullptr, EPI_STORE));
+        RUN(swiglu_f32(f.G, f.U, f.Hb, (int64_t)M * F, s));
+        RUN(gemm(f.Hb, F, ly.wdown, f.X, D, M, D, F, nullptr, EPI_GATED_RES, md + 5 * D));
+    }
+    // norm_out AdaLN + proj_out + crop (base:1491-1501)
+    RUN(rmsnorm_f32(f.X, f.norm_out, f.mod_out, f.mod_out + D, 2 * D, S, f.XN, M, D, eps, s));
+    RUN(gemm(f.XN, D, f.wout, T % 2 == 0 ? vt_out : f.O2, 128, M, 128, D, f.bout, EPI_STORE));
+    if (T % 2) RUN(crop_rows_f32(f.O2, Bc, 2 * S, T, 64, vt_out, s));
+#undef RUN
+    return 0;
+}

@@ -113,6 +113,48 @@ int fsq_quantize(const bf16_t *z, int64_t ldz, int M, const FsqLevels &lv, bf16_
                  hipStream_t s);
 int fsq_codes_from_indices(const int *idx, int M, const FsqLevels &lv, bf16_t *codes, int64_t ldc, hipStream_t s);
 
+// ------------------------------------------------------ fp32 parity mode ---
+// (f32.hip) the DiT forward with no bf16 rounding, SURVEY §8c(iii)
+struct GemmF32Args {
+    const float *A; int64_t lda;     // [M, K]
+    const float *W; int64_t ldw;     // [N, K]
+    float *C; int64_t ldc;
+    int M, N, K;
+    int epi;                          // EPI_STORE / EPI_GATED_RES / EPI_RES
+    const float *bias;
+    const float *res; int64_t ldr;
+    const float *gate; int64_t gate_bstride; int rows_per_batch;
+};
+int gemm_f32(const GemmF32Args &a, hipStream_t s);
+struct HeadPostF32Args {
+    const float *src; int64_t ld_src;
+    int B, S, nq, nk, nv;
+    const float *qw, *kw, *cos, *sin;
+    float *q, *k, *v;
+    int S_dst;
+    float eps;
+};
+int head_post_f32(const HeadPostF32Args &a, hipStream_t s);
+struct AttnF32Args {
+    const float *q, *k, *v;           // [B][H|KV][S][128]
+    float *o; int64_t o_ld;           // [B][Sq][o_ld], head h at column h·128
+    int B, H, KV, Sq, Sk, window;
+    float scale;
+};
+int attention_f32(const AttnF32Args &a, hipStream_t s);
+int rmsnorm_f32(const float *x, const float *w, const float *shift, const float *scale, int64_t mod_bstride,
+                int rows_per_batch, float *out, int M, int D, float eps, hipStream_t s);
+int gemv_f32(const float *x, int64_t ldx, const float *W, const float *bias, float *y, int64_t ldy, int M, int N,
+             int K, int act, hipStream_t s);
+int timestep_sinusoid_f32(const float *t, const float *t_r, int t_stride, int use_diff, int Bc, const float *freqs,
+                          float *emb, hipStream_t s);
+int add_f32(const float *a, const float *b, float *o, int64_t n, hipStream_t s);
+int modulation_f32(const float *tables, int n_tables, int rows, const float *proj, int Bc, int D, float *mod,
+                   hipStream_t s);
+int pack_patches_f32(const float *xt, const float *ctx, int Bx, int Bc, int T, int S, float *X, hipStream_t s);
+int crop_rows_f32(const float *src, int Bc, int rows_src, int rows_dst, int C, float *dst, hipStream_t s);
+int swiglu_f32(const float *g, const float *u, float *o, int64_t n, hipStream_t s);
+
 // ----------------------------------------------------------------- misc ----
 // per song b: peak = max |wav[b]|; if peak > 1, wav[b] /= peak (n samples per song, n % 4 == 0)
 // decode guard (when guard != 0) then normalize_audio (when target_amp > 0), see small.hip

@@ -68,6 +68,10 @@ typedef struct acehip_dit_cfg {
     int max_Bc;          /* max DiT batch (2x songs with CFG) */
     int max_Lenc;        /* max encoder sequence length */
     const uint8_t *sliding; /* [layers] 1 = sliding layer; NULL = even idx */
+    int fp32;            /* 0: the bf16 production path; 1: the fp32 parity mode (SURVEY
+                          * §8c(iii)) — fp32 weights, activations and accumulation, the
+                          * reference's fp32 forward (init_service_orchestrator.py:51 runs
+                          * fp32 off cuda/xpu); set_condition / forward then take fp32 */
 } acehip_dit_cfg;
 
 typedef struct acehip_dit acehip_dit;
@@ -89,7 +93,7 @@ int acehip_dit_finalize(acehip_dit *h);
 /* condition_embedder + per-layer cross-attention K/V cache.
  * replaces: the first-step branch of AceStepAttention.forward
  * (acestep/models/base/modeling_acestep_v15_base.py:310-325, :1359).
- * enc: bf16 [Bc, Lenc, hidden] (CFG: cond rows then null rows). */
+ * enc: [Bc, Lenc, hidden] in the handle's dtype (CFG: cond rows then null rows). */
 int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, void *stream);
 
 /* Declare batch rows [first_row, Bc) of the current condition uniform: their
@@ -106,11 +110,13 @@ int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream);
  * (acestep/models/base/modeling_acestep_v15_base.py:1303-1507).
  * xt: bf16 [Bx, T, 64]; ctx: bf16 [Bx, T, 128]; batch row b of the DiT reads
  * xt/ctx row (b % Bx) — CFG's cat([xt, xt]) without a copy (base:1929).
- * t, t_r: device fp32 [Bc] holding bf16-representable values; t_stride 0
- * broadcasts element 0.  vt_out: bf16 [Bc, T, 64]. */
+ * t, t_r: device fp32 [Bc] holding model-dtype values; t_stride 0
+ * broadcasts element 0.  vt_out: [Bc, T, 64].  dtype is the
+ * element type of xt / ctx / vt_out and must be the handle's: ACEHIP_BF16
+ * (production) or ACEHIP_F32 (a handle created with cfg.fp32 = 1). */
 int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx,
                        const float *t, const float *t_r, int t_stride, int Bc, int T,
-                       void *vt_out, void *stream);
+                       int dtype, void *vt_out, void *stream);
 
 /* Replay the pointer-independent middle of acehip_dit_forward (timestep MLPs,
  * modulation, proj_in, the layer stack, norm_out) as one HIP graph, captured

@@ -37,7 +37,7 @@ def test_error_paths_without_gpu():
     assert rc == -1 and b"head_dim" in lib.acehip_last_error()
     with pytest.raises(RuntimeError, match="head_dim"):
         _ffi.check(rc, "dit_create")
-    assert lib.acehip_dit_forward(None, None, None, 1, None, None, 0, 2, 10, None, None) == -1
+    assert lib.acehip_dit_forward(None, None, None, 1, None, None, 0, 2, 10, _ffi.ACEHIP_BF16, None, None) == -1
     assert lib.acehip_vae_decode(None, None, 1, 1, None, None) == -1
 
 
