@@ -75,9 +75,9 @@ def _declare(lib):
         "acehip_dit_profile_kinds": (c_int, [P, ctypes.c_uint]),
         "acehip_dit_profile_read": (c_int, [P, c_int, POINTER(c_int), POINTER(c_float)]),
         "acehip_sampler_apg_euler": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, c_int,
-                                             c_int, c_int, P]),
-        "acehip_sampler_adg_euler": (c_int, [P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_int, P]),
-        "acehip_sampler_axpy": (c_int, [P, P, c_int64, c_float, P]),
+                                             c_int, c_int, c_int, P]),
+        "acehip_sampler_adg_euler": (c_int, [P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_int, P]),
+        "acehip_sampler_axpy": (c_int, [P, P, c_int64, c_float, c_int, P]),
         "acehip_vae_create": (c_int, [c_int, POINTER(VAECfg), POINTER(c_void_p)]),
         "acehip_vae_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
         "acehip_vae_finalize": (c_int, [P]),
@@ -142,6 +142,16 @@ def stream_ptr(stream=None):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return c_void_p(s.cuda_stream)
+
+
+def dtype_code(t) -> int:
+    """ACEHIP_F32 / ACEHIP_BF16 of a tensor (anything else is refused)."""
+    import torch
+    if t.dtype == torch.float32:
+        return ACEHIP_F32
+    if t.dtype == torch.bfloat16:
+        return ACEHIP_BF16
+    raise TypeError(f"acehip: unsupported dtype {t.dtype}")
 
 
 def ptr(t):

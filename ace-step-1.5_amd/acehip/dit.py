@@ -172,11 +172,18 @@ class DiTRuntime:
             pass
 
 
+def _same_dtype(*ts):
+    d = ts[0].dtype
+    assert all(t is None or (t.dtype == d and t.is_contiguous()) for t in ts), [t.dtype for t in ts if t is not None]
+    return _ffi.dtype_code(ts[0])
+
+
 def apg_euler_(vt, xt, ra, guidance, dt, apply_cfg, first_step, out_mode=0):
-    """Fused CFG split + APG + Euler (in place on xt).  vt [2B|B, T, 64]."""
+    """Fused CFG split + APG + Euler (in place on xt).  vt [2B|B, T, 64]; bf16 or fp32."""
     B, T, C = xt.shape
+    dt_code = _same_dtype(xt, vt, ra)
     check(lib().acehip_sampler_apg_euler(ptr(vt), ptr(xt), ptr(ra), B, T, C, float(guidance),
-                                         float(dt), int(apply_cfg), int(first_step), int(out_mode),
+                                         float(dt), int(apply_cfg), int(first_step), int(out_mode), dt_code,
                                          stream_ptr()), "sampler_apg_euler")
 
 
@@ -184,13 +191,15 @@ def adg_euler_(vt, xt, guidance, sigma, dt, out_mode=0):
     """Fused CFG split + ADG + Euler (in place on xt).  vt [2B, T, 64]; with
     out_mode=1 xt must hold the latents on entry and receives the guided v."""
     B, T, C = xt.shape
+    dt_code = _same_dtype(xt, vt)
     check(lib().acehip_sampler_adg_euler(ptr(vt), ptr(xt), B, T, C, float(guidance), float(sigma),
-                                         float(dt), int(out_mode), stream_ptr()), "sampler_adg_euler")
+                                         float(dt), int(out_mode), dt_code, stream_ptr()), "sampler_adg_euler")
 
 
 def axpy_(vt, xt, s):
-    """xt = bf16(xt − bf16(vt·s)) in place."""
-    check(lib().acehip_sampler_axpy(ptr(vt), ptr(xt), xt.numel(), float(s), stream_ptr()), "axpy")
+    """xt = xt − vt·s in place, each op rounded to the storage dtype."""
+    dt_code = _same_dtype(xt, vt)
+    check(lib().acehip_sampler_axpy(ptr(vt), ptr(xt), xt.numel(), float(s), dt_code, stream_ptr()), "axpy")
 
 
 def prepare_noise(shape, device, dtype, seed):
@@ -253,7 +262,9 @@ class AceStepDiTBackend:
                  prepare_condition=None, dtype=torch.bfloat16, accepts_timesteps: Optional[bool] = None):
         self.rt = runtime
         self.device = runtime.device
-        self.dtype = dtype
+        if getattr(runtime, "dtype", dtype) != dtype:
+            raise ValueError(f"AceStepDiTBackend: runtime dtype {runtime.dtype} != {dtype}")
+        self.dtype = dtype          # bf16: production; fp32: the parity mode (DiTRuntime(dtype=fp32))
         self.null = null_condition_emb.detach().to(self.device, dtype)
         self.is_turbo = is_turbo
         # custom ``timesteps``: the turbo (turbo:1803,1828-1857) and sft (sft:1811,1866-1868)
@@ -279,11 +290,13 @@ class AceStepDiTBackend:
                         layer_types=list(c.layer_types))
         dev = next(model.parameters()).device
         max_S = int(max_seconds * 25 + 1) // 2 + 1
-        rt = DiTRuntime(cfg, dev.index or 0, max_S=max_S, max_Bc=2 * max_batch, max_Lenc=max_Lenc)
+        dtype = next(model.parameters()).dtype
+        rt = DiTRuntime(cfg, dev.index or 0, max_S=max_S, max_Bc=2 * max_batch, max_Lenc=max_Lenc,
+                        dtype=torch.float32 if dtype == torch.float32 else torch.bfloat16)
         rt.load(model.decoder.state_dict())
         turbo = bool(getattr(c, "is_turbo", False)) or getattr(c, "model_version", "") == "turbo"
         return cls(rt, model.null_condition_emb, is_turbo=turbo,
-                   prepare_condition=model.prepare_condition, dtype=next(model.parameters()).dtype,
+                   prepare_condition=model.prepare_condition, dtype=rt.dtype,
                    accepts_timesteps=turbo or takes_timesteps(model))
 
     # ------------------------------------------------------------------ API --

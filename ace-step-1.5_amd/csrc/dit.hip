@@ -737,23 +737,33 @@ int acehip_dit_destroy(acehip_dit *h) {
     return 0;
 }
 
+static int sampler_dtype(int dtype, bool *f32) {
+    if (dtype != ACEHIP_BF16 && dtype != ACEHIP_F32) return fail(ACEHIP_E_ARG, "sampler: dtype");
+    *f32 = dtype == ACEHIP_F32;
+    return 0;
+}
+
 int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float guidance,
-                             float dt, int apply_cfg, int first_step, int out_mode, void *stream) {
+                             float dt, int apply_cfg, int first_step, int out_mode, int dtype, void *stream) {
     if (!vt || !xt || (apply_cfg > 0 && !ra)) return fail(ACEHIP_E_ARG, "null argument");
-    return apg_euler((const bf16_t *)vt, (bf16_t *)xt, (bf16_t *)ra, B, T, C, guidance, dt, apply_cfg,
-                     first_step, out_mode, (hipStream_t)stream);
+    bool f32;
+    if (int rc = sampler_dtype(dtype, &f32)) return rc;
+    return apg_euler(vt, xt, ra, B, T, C, guidance, dt, apply_cfg, first_step, out_mode, f32, (hipStream_t)stream);
 }
 
 int acehip_sampler_adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, float sigma,
-                             float dt, int out_mode, void *stream) {
+                             float dt, int out_mode, int dtype, void *stream) {
     if (!vt || !xt) return fail(ACEHIP_E_ARG, "null argument");
-    return adg_euler((const bf16_t *)vt, (bf16_t *)xt, B, T, C, guidance, sigma, dt, out_mode,
-                     (hipStream_t)stream);
+    bool f32;
+    if (int rc = sampler_dtype(dtype, &f32)) return rc;
+    return adg_euler(vt, xt, B, T, C, guidance, sigma, dt, out_mode, f32, (hipStream_t)stream);
 }
 
-int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream) {
+int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, int dtype, void *stream) {
     if (!vt || !xt) return fail(ACEHIP_E_ARG, "null argument");
-    return axpy_bf16((const bf16_t *)vt, (bf16_t *)xt, n, s, (hipStream_t)stream);
+    bool f32;
+    if (int rc = sampler_dtype(dtype, &f32)) return rc;
+    return axpy(vt, xt, n, s, f32, (hipStream_t)stream);
 }
 
 int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,

@@ -100,11 +100,12 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
 size_t attention_ws_bytes();
 
 // --------------------------------------------------------------- sampler ---
-int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,
-              float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s);
-int axpy_bf16(const bf16_t *vt, bf16_t *xt, int64_t n, float sc, hipStream_t s);
-int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance, float sigma,
-              float dt, int out_mode, hipStream_t s);
+// element type bf16 (f32 = false) or fp32 (the parity mode)
+int apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float guidance, float dt, int apply_cfg,
+              int first_step, int out_mode, bool f32, hipStream_t s);
+int axpy(const void *vt, void *xt, int64_t n, float sc, bool f32, hipStream_t s);
+int adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, float sigma, float dt, int out_mode,
+              bool f32, hipStream_t s);
 
 // ------------------------------------------------------------------ FSQ ----
 struct FsqLevels { int n; int L[8]; };

@@ -6,6 +6,8 @@
 //   ‖ra‖₂ over T per channel → bf16; sf = min(1, bf16(2.5/‖ra‖)); v0 = bf16(ra·sf)
 //   v1 = cond/max(‖cond‖,1e-12); par = Σ(v0·v1)·v1; orth = v0 − par   (float64)
 //   vt = bf16(cond + bf16((g−1)·bf16(orth)));  xt = bf16(xt − bf16(vt·dt))
+// Storage type S = bf16 (production: every op output rounded to bf16 as torch
+// does) or float (the fp32 parity mode: the same chain with no rounding).
 // The norms are global per-(song, channel) reductions over T, so one
 // thread workgroup (512 threads) owns 8 channels of one song (16-B row accesses) and runs
 // three L2-resident passes with LDS reductions in between: no host sync, no
@@ -15,11 +17,31 @@
 namespace acehip {
 namespace {
 
+// 8 consecutive elements of a row: bf16 (16 B) or fp32 (32 B); R = the storage
+// type's rounding of one op output (torch's bf16 op semantics / none in fp32)
+__device__ __forceinline__ void ld8(const bf16_t *p, float *f) { unpack8(*(const uint4 *)p, f); }
+__device__ __forceinline__ void ld8(const float *p, float *f) {
+    const float4 a = *(const float4 *)p, b = *(const float4 *)(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t *p, const float *f) { *(uint4 *)p = pack8(f); }
+__device__ __forceinline__ void st8(float *p, const float *f) {
+    *(float4 *)p = make_float4(f[0], f[1], f[2], f[3]);
+    *(float4 *)(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+}
+template <class S> __device__ __forceinline__ float R(float x) { return rbf(x); }
+template <> __device__ __forceinline__ float R<float>(float x) { return x; }
+__device__ __forceinline__ float ld1(const bf16_t *p) { return bf2f(*p); }
+__device__ __forceinline__ float ld1(const float *p) { return *p; }
+__device__ __forceinline__ void st1(bf16_t *p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void st1(float *p, float v) { *p = v; }
+
 // grid (8 channel groups, B songs); 512 threads = 512 rows in flight, each
 // thread owns 8 consecutive channels (one 16-B access per row)
-__global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict__ vt,
-                                                         bf16_t *__restrict__ xt,
-                                                         bf16_t *__restrict__ ra, int B, int T,
+template <class S>
+__global__ __launch_bounds__(512) void apg_euler_kernel(const S *__restrict__ vt,
+                                                         S *__restrict__ xt,
+                                                         S *__restrict__ ra, int B, int T,
                                                          float guidance, float dt, int apply_cfg,
                                                          int first_step, int out_mode) {
     constexpr int C = 64, CG = 8, NTH = 512, NW = NTH / 64;
@@ -28,25 +50,24 @@ __global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict
     const int cg = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t base = (int64_t)b * T * C + cg * CG;
-    const bf16_t *cond = vt + base;
-    const bf16_t *unc = vt + (int64_t)B * T * C + base;
-    bf16_t *x = xt + base;
+    const S *cond = vt + base;
+    const S *unc = vt + (int64_t)B * T * C + base;
+    S *x = xt + base;
     if (apply_cfg <= 0) {
         // no CFG (vt is [B,T,C]) or outside the CFG interval (vt = cond)
         for (int t = tid; t < T; t += NTH) {
             const int64_t i = (int64_t)t * C;
             float c8[8], x8[8];
-            const uint4 cr = *(const uint4 *)(cond + i);
-            if (out_mode) { *(uint4 *)(x + i) = cr; continue; }
-            unpack8(cr, c8);
-            unpack8(*(const uint4 *)(x + i), x8);
+            ld8(cond + i, c8);
+            if (out_mode) { st8(x + i, c8); continue; }
+            ld8(x + i, x8);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x8[j] = x8[j] - rbf(c8[j] * dt);
-            *(uint4 *)(x + i) = pack8(x8);
+            for (int j = 0; j < 8; ++j) x8[j] = R<S>(x8[j] - R<S>(c8[j] * dt));
+            st8(x + i, x8);
         }
         return;
     }
-    bf16_t *rab = ra + base;
+    S *rab = ra + base;
     float ss[8];
     double cs[8];
 #pragma unroll
@@ -54,17 +75,17 @@ __global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict
     for (int t = tid; t < T; t += NTH) {
         const int64_t i = (int64_t)t * C;
         float c8[8], u8[8], r8[8];
-        unpack8(*(const uint4 *)(cond + i), c8);
-        unpack8(*(const uint4 *)(unc + i), u8);
-        if (!first_step) unpack8(*(const uint4 *)(rab + i), r8);
+        ld8(cond + i, c8);
+        ld8(unc + i, u8);
+        if (!first_step) ld8(rab + i, r8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float diff = rbf(c8[j] - u8[j]);
-            r8[j] = first_step ? diff : rbf(diff + rbf(-0.75f * r8[j]));
+            const float diff = R<S>(c8[j] - u8[j]);
+            r8[j] = first_step ? diff : R<S>(diff + R<S>(-0.75f * r8[j]));
             ss[j] += r8[j] * r8[j];
             cs[j] += (double)c8[j] * (double)c8[j];
         }
-        *(uint4 *)(rab + i) = pack8(r8);
+        st8(rab + i, r8);
     }
     // block reduction per channel
 #pragma unroll
@@ -83,8 +104,8 @@ __global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict
         float a = 0.f;
         double c = 0.0;
         for (int w = 0; w < NW; ++w) { a += s_ss[w][j]; c += s_cs[w][j]; }
-        const float nrm = rbf(sqrtf(a));
-        sf[j] = fminf(1.0f, rbf(2.5f / nrm));
+        const float nrm = R<S>(sqrtf(a));
+        sf[j] = fminf(1.0f, R<S>(2.5f / nrm));
         denom[j] = fmax(sqrt(c), 1e-12);
         dot[j] = 0.0;
     }
@@ -92,10 +113,10 @@ __global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict
     for (int t = tid; t < T; t += NTH) {
         const int64_t i = (int64_t)t * C;
         float c8[8], r8[8];
-        unpack8(*(const uint4 *)(cond + i), c8);
-        unpack8(*(const uint4 *)(rab + i), r8);
+        ld8(cond + i, c8);
+        ld8(rab + i, r8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dot[j] += (double)rbf(r8[j] * sf[j]) * ((double)c8[j] / denom[j]);
+        for (int j = 0; j < 8; ++j) dot[j] += (double)R<S>(r8[j] * sf[j]) * ((double)c8[j] / denom[j]);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) dot[j] = wave_sum_d(dot[j]);
@@ -113,32 +134,33 @@ __global__ __launch_bounds__(512) void apg_euler_kernel(const bf16_t *__restrict
     for (int t = tid; t < T; t += NTH) {
         const int64_t i = (int64_t)t * C;
         float c8[8], r8[8], x8[8];
-        unpack8(*(const uint4 *)(cond + i), c8);
-        unpack8(*(const uint4 *)(rab + i), r8);
-        if (!out_mode) unpack8(*(const uint4 *)(x + i), x8);
+        ld8(cond + i, c8);
+        ld8(rab + i, r8);
+        if (!out_mode) ld8(x + i, x8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const double v0 = (double)rbf(r8[j] * sf[j]);
+            const double v0 = (double)R<S>(r8[j] * sf[j]);
             const double v1 = (double)c8[j] / denom[j];
-            const float orth = rbf((float)(v0 - dot[j] * v1));
-            const float g = rbf(c8[j] + rbf(gm1 * orth));
-            x8[j] = out_mode ? g : x8[j] - rbf(g * dt);
+            const float orth = R<S>((float)(v0 - dot[j] * v1));
+            const float g = R<S>(c8[j] + R<S>(gm1 * orth));
+            x8[j] = out_mode ? g : R<S>(x8[j] - R<S>(g * dt));
         }
-        *(uint4 *)(x + i) = pack8(x8);
+        st8(x + i, x8);
     }
 }
 
-__global__ void axpy_kernel(const bf16_t *vt, bf16_t *xt, int64_t n, float sc) {
+template <class S>
+__global__ void axpy_kernel(const S *vt, S *xt, int64_t n, float sc) {
     const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
     if (i + 8 <= n) {
         float v[8], x[8];
-        unpack8(*(const uint4 *)(vt + i), v);
-        unpack8(*(const uint4 *)(xt + i), x);
+        ld8(vt + i, v);
+        ld8(xt + i, x);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = x[j] - rbf(v[j] * sc);
-        *(uint4 *)(xt + i) = pack8(x);
+        for (int j = 0; j < 8; ++j) x[j] = R<S>(x[j] - R<S>(v[j] * sc));
+        st8(xt + i, x);
     } else {
-        for (int64_t k = i; k < n; ++k) xt[k] = f2bf(bf2f(xt[k]) - rbf(bf2f(vt[k]) * sc));
+        for (int64_t k = i; k < n; ++k) st1(xt + k, R<S>(ld1(xt + k) - R<S>(ld1(vt + k) * sc)));
     }
 }
 
@@ -151,20 +173,21 @@ __global__ void axpy_kernel(const bf16_t *vt, bf16_t *xt, int64_t n, float sc) {
 // dot); the perpendicular split in float32; the recombination in float64
 // (masks applied by multiplication, so a 0/0 stays NaN exactly as in torch);
 // the result cast float64 → float32 → bf16 (c10's double → BFloat16 path).
-__global__ __launch_bounds__(256) void adg_euler_kernel(const bf16_t *__restrict__ vt,
-                                                        bf16_t *__restrict__ xt, int B, int T,
+template <class S>
+__global__ __launch_bounds__(256) void adg_euler_kernel(const S *__restrict__ vt,
+                                                        S *__restrict__ xt, int B, int T,
                                                         float guidance, float sigma, float dt,
                                                         int out_mode) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= (int64_t)B * T) return;
     const int64_t i = row * 64 + lane;
-    const float x = bf2f(xt[i]);
-    const float vc = bf2f(vt[i]);
-    const float vu = bf2f(vt[(int64_t)B * T * 64 + i]);
-    const float ht = rbf(x - rbf(sigma * vc));
-    const float hu = rbf(x - rbf(sigma * vu));
-    const float diff = rbf(ht - hu);
+    const float x = ld1(xt + i);
+    const float vc = ld1(vt + i);
+    const float vu = ld1(vt + (int64_t)B * T * 64 + i);
+    const float ht = R<S>(x - R<S>(sigma * vc));
+    const float hu = R<S>(x - R<S>(sigma * vu));
+    const float diff = R<S>(ht - hu);
     // angle, float64
     const double na = sqrt(wave_sum_d((double)ht * (double)ht));
     const double nb = sqrt(wave_sum_d((double)hu * (double)hu));
@@ -184,36 +207,45 @@ __global__ __launch_bounds__(256) void adg_euler_kernel(const bf16_t *__restrict
     const double p1 = (double)perp * sn / st * (st > 1e-3 ? 1.0 : 0.0);
     const float p2 = perp * (float)w * (st <= 1e-3 ? 1.0f : 0.0f);
     const double nw = v_new + (p1 + (double)p2);
-    const float v = rbf((float)(((double)x - nw) / (double)sigma));
-    xt[i] = f2bf(out_mode ? v : x - rbf(v * dt));
+    const float v = R<S>((float)(((double)x - nw) / (double)sigma));
+    st1(xt + i, out_mode ? v : R<S>(x - R<S>(v * dt)));
 }
 
 }  // namespace
 
-int adg_euler(const bf16_t *vt, bf16_t *xt, int B, int T, int C, float guidance, float sigma,
-              float dt, int out_mode, hipStream_t s) {
+int adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, float sigma, float dt, int out_mode,
+              bool f32, hipStream_t s) {
     if (C != 64) return fail(-1, "adg_euler: C must be 64");
     if (B <= 0 || T <= 0) return 0;
     const int64_t rows = (int64_t)B * T;
-    adg_euler_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(vt, xt, B, T, guidance, sigma, dt, out_mode);
+    const unsigned g = (unsigned)((rows + 3) / 4);
+    if (f32) adg_euler_kernel<float><<<g, 256, 0, s>>>((const float *)vt, (float *)xt, B, T, guidance, sigma, dt, out_mode);
+    else adg_euler_kernel<bf16_t><<<g, 256, 0, s>>>((const bf16_t *)vt, (bf16_t *)xt, B, T, guidance, sigma, dt, out_mode);
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-int apg_euler(const bf16_t *vt, bf16_t *xt, bf16_t *ra, int B, int T, int C, float guidance,
-              float dt, int apply_cfg, int first_step, int out_mode, hipStream_t s) {
+int apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float guidance, float dt, int apply_cfg,
+              int first_step, int out_mode, bool f32, hipStream_t s) {
     if (C != 64) return fail(-1, "apg_euler: C must be 64");
     if (B <= 0 || T <= 0) return 0;
-    apg_euler_kernel<<<dim3(C / 8, B), 512, 0, s>>>(vt, xt, ra, B, T, guidance, dt, apply_cfg, first_step,
-                                                     out_mode);
+    const dim3 g(C / 8, B);
+    if (f32)
+        apg_euler_kernel<float><<<g, 512, 0, s>>>((const float *)vt, (float *)xt, (float *)ra, B, T, guidance, dt,
+                                                  apply_cfg, first_step, out_mode);
+    else
+        apg_euler_kernel<bf16_t><<<g, 512, 0, s>>>((const bf16_t *)vt, (bf16_t *)xt, (bf16_t *)ra, B, T, guidance, dt,
+                                                   apply_cfg, first_step, out_mode);
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-int axpy_bf16(const bf16_t *vt, bf16_t *xt, int64_t n, float sc, hipStream_t s) {
+int axpy(const void *vt, void *xt, int64_t n, float sc, bool f32, hipStream_t s) {
     if (n <= 0) return 0;
     const int64_t threads = (n + 7) / 8;
-    axpy_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(vt, xt, n, sc);
+    const unsigned g = (unsigned)((threads + 255) / 256);
+    if (f32) axpy_kernel<float><<<g, 256, 0, s>>>((const float *)vt, (float *)xt, n, sc);
+    else axpy_kernel<bf16_t><<<g, 256, 0, s>>>((const bf16_t *)vt, (bf16_t *)xt, n, sc);
     HIP_TRY(hipGetLastError());
     return 0;
 }

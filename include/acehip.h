@@ -210,10 +210,12 @@ int acehip_fsq_codes_from_indices(const int32_t *indices, int M, const int *leve
  * means running_average == 0); apply_cfg == 0 → vt = cond (no momentum
  * update), apply_cfg < 0 → no CFG (vt is [B,T,64]).  dt: bf16 value.
  * out_mode 0: xt = bf16(xt − bf16(v·dt)) (ODE);  out_mode 1: xt = v (the
- * guided velocity, for the caller's SDE branch, base:1968-1973). */
+ * guided velocity, for the caller's SDE branch, base:1968-1973).
+ * dtype: ACEHIP_BF16 (every op rounded to bf16 as torch does) or ACEHIP_F32 (the
+ * fp32 parity mode: the same chain unrounded) for vt / xt / ra. */
 int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C,
                              float guidance, float dt, int apply_cfg, int first_step,
-                             int out_mode, void *stream);
+                             int out_mode, int dtype, void *stream);
 
 /* One base/sft CFG step with ADG guidance (use_adg=True) + Euler, fused.
  * replaces: base:1958-1964 + adg_forward (apg_guidance.py:107-180, angle clip
@@ -222,11 +224,11 @@ int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, i
  * T).  The reference only supports B == 1 (its [N*T,1] x [N,T,C] broadcast);
  * this computes the per-row generalisation for any B.  out_mode as above. */
 int acehip_sampler_adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance,
-                             float sigma, float dt, int out_mode, void *stream);
+                             float sigma, float dt, int out_mode, int dtype, void *stream);
 
 /* xt = bf16(xt - bf16(vt * s)) on [n] elements — Euler ODE (turbo:1985-1991)
- * and the final x0 = xt - vt*t (turbo:1975-1977). */
-int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, void *stream);
+ * and the final x0 = xt - vt*t (turbo:1975-1977); dtype as above. */
+int acehip_sampler_axpy(const void *vt, void *xt, int64_t n, float s, int dtype, void *stream);
 
 /* ---------------------------------------------------------------- VAE ---- */
 

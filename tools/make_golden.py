@@ -364,6 +364,15 @@ def main_only(which):
         sm["turbo_sde"] = gen_sampler("turbo", "turbo_sde", bf, 2, 40, shift=1.0, infer_method="sde")
         sm["sft_timesteps"] = gen_sampler("sft", "sft_timesteps", bf, 1, 40, diffusion_guidance_sale=7.0,
                                           shift=3.0, timesteps=torch.tensor([1.0, 0.9, 0.7, 0.5, 0.3, 0.1, 0.0]))
+    if "sampler_fp32" in which:
+        # the fp32 parity mode of the samplers (the reference's fp32 path off cuda/xpu)
+        f32 = torch.float32
+        sm = manifest["sampler"]
+        sm["base_s8_sh3_fp32"] = gen_sampler("base", "base_s8_sh3_fp32", f32, 2, 40, infer_steps=8, shift=3.0,
+                                             diffusion_guidance_sale=7.0)
+        sm["base_s8_adg_fp32"] = gen_sampler("base", "base_s8_adg_fp32", f32, 1, 40, infer_steps=8, shift=3.0,
+                                             diffusion_guidance_sale=7.0, use_adg=True)
+        sm["turbo_sh3_fp32"] = gen_sampler("turbo", "turbo_sh3_fp32", f32, 2, 40, shift=3.0)
     if "long" in which:
         # full width with S > 2W+1 so the ±128 band of the even layers is pinned at full
         # width against the reference (base:56-135, :1378-1447); odd T (pad + crop)
