@@ -48,6 +48,13 @@ namespace {
 #ifndef ATT_PRIO
 #define ATT_PRIO 1         // static s_setprio 1 for the deferred (younger) half
 #endif
+#ifndef ATT_TAU
+#define ATT_TAU 8.0f       // lazy-rescale threshold (0: rescale on every new max)
+#endif
+#ifndef ATT_RING3
+#define ATT_RING3 0        // 3-deep K/V ring: tile j+2 in flight behind a counted vmcnt across the
+#endif                     // barrier (the 2-deep ring drained the DMA queue with vmcnt(0) every tile)
+static_assert(!(ATT_DEFER && ATT_RING3), "the deferred P·V reads V(j-1), which the 3-deep ring refills");
 
 constexpr int QB = 128;    // queries per workgroup
 constexpr int KT = 64;     // keys per tile
@@ -68,6 +75,43 @@ struct SplitArgs {
     int *cnt;      // ≥ units − full ints, zero between launches
 };
 
+// ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
+__device__ __forceinline__ s16x4 ds_read_tr16(const char *lds_ptr) {
+    s16x4 r;
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds_ptr;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
+__device__ __forceinline__ bf16x8 ds_read_b128(const char *lds_ptr) {
+    bf16x8 r;
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds_ptr;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+// LDS reads at (per-lane offset + wave-uniform offset): the uniform part (ring slot, row
+// block) lives in an SGPR and is added inside the asm, so the compiler cannot hoist one
+// VGPR address per (slot, fragment) out of the tile loop — that costs ~50 VGPRs it has
+// to spill.  The per-lane parts (swizzled chunk offsets) are 8 VGPRs for K, 8 for V.
+__device__ __forceinline__ bf16x8 ds_read_b128_at(uint32_t lane_off, uint32_t uni_off) {
+    bf16x8 r;
+    uint32_t a;
+    asm volatile("v_add_u32 %1, %2, %3\n\tds_read_b128 %0, %1" : "=v"(r), "=&v"(a) : "s"(uni_off), "v"(lane_off));
+    return r;
+}
+__device__ __forceinline__ s16x4 ds_read_tr16_at(uint32_t lane_off, uint32_t uni_off) {
+    s16x4 r;
+    uint32_t a;
+    asm volatile("v_add_u32 %1, %2, %3\n\tds_read_b64_tr_b16 %0, %1" : "=v"(r), "=&v"(a) : "s"(uni_off), "v"(lane_off));
+    return r;
+}
+// s_waitcnt lgkmcnt(0) that the listed fragments depend on (nothing using them can be
+// scheduled above it)
+__device__ __forceinline__ void lgkm_wait8(bf16x8 (&f)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]),
+                 "+v"(f[6]), "+v"(f[7]));
+}
+
 __device__ __forceinline__ int kvoff(int row, int ch) {
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
@@ -85,7 +129,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const uint8_t *__restrict__ kmask) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
-    constexpr int NBUF = ATT_DEFER ? 3 : 2;        // K/V ring (deferred P·V still reads V(j−1))
+    constexpr int NBUF = (ATT_DEFER || ATT_RING3) ? 3 : 2;   // K/V ring (deferred P·V still reads V(j−1))
+    constexpr int GPW = 32 / (NT / 64);            // LDS-DMA instructions per wave per tile
     __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
@@ -119,6 +164,11 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     bf16x8 qf[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8 *)(qp + 16 * s + 8 * hh);
+    // retire the Q loads with a waitcnt the compiler SEES (builtin, not asm: vmcnt(0)
+    // expcnt(7) lgkmcnt(15)); otherwise its waitcnt pass, which cannot tell the loop's
+    // LDS-DMAs from these register loads, re-waits vmcnt(0) at the first use of qf in
+    // every tile — draining the K/V ring (cdna_hip_programming.md §5 trap (b))
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 
     const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
     const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
@@ -165,39 +215,92 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
 
     const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
-    // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads
+    // LDS byte address of the ring (uniform) and the per-lane swizzled offsets:
+    // K fragment (row r [+32], logical chunk 2s+hh) — the swizzle depends on row & 15 only;
+    // Vᵀ fragment (d-block dt, row 4(g>>1)+qq [+8]) — rows +16s, +32t are uniform offsets
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    uint32_t koff[8], voff[4][2];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) koff[s] = kvoff(r, 2 * s + hh);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int h8 = 0; h8 < 2; ++h8)
+            voff[dt][h8] = kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+    // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads.  The reads are issued by
+    // inline asm: hipcc's waitcnt pass treats its own ds_read_tr builtin as an LDS read
+    // that may alias the in-flight LDS-DMA refills and waits vmcnt(0) before it (every
+    // tile, draining the ring); the asm reads are waited explicitly (lgkmcnt(0) bound to
+    // their results, so no MFMA can move above the wait)
+    auto pv_reads = [&](uint32_t vbase, int dt, s16x4 (&rd)[2][2][2]) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const uint32_t ub = vbase + (32 * t + 16 * s) * 256;
+                rd[t][s][0] = ds_read_tr16_at(voff[dt][0], ub);
+                rd[t][s][1] = ds_read_tr16_at(voff[dt][1], ub);
+            }
+    };
+    auto pv_wait = [](s16x4 (&rd)[2][2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(rd[0][0][0]), "+v"(rd[0][0][1]), "+v"(rd[0][1][0]), "+v"(rd[0][1][1]),
+                       "+v"(rd[1][0][0]), "+v"(rd[1][0][1]), "+v"(rd[1][1][0]), "+v"(rd[1][1][1]));
+    };
+    auto pv_mfma = [&](int dt, const s16x4 (&rd)[2][2][2], const bf16x8 (&pf)[2][2]) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                // whole-vector reinterpretation (per-element bit_cast<__bf16> insertion
+                // is miscompiled by ROCm 7.2 hipcc: it keeps only the first dword)
+                const s16x8 cat = __builtin_shufflevector(rd[t][s][0], rd[t][s][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                const bf16x8 vf = __builtin_bit_cast(bf16x8, cat);
+                oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
+            }
+    };
+    // P·V: the reads of d-block dt+1 are in flight during the MFMAs of dt
+    // ldsV: the V half of a ring slot (uniform)
     auto pv = [&](const char *ldsV, const bf16x8 (&pf)[2][2]) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            const int dc = 32 * dt + 16 * (g & 1);
-            const int chk = (dc >> 3) + (pp >> 1);
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int kb = 32 * t + 16 * s + 4 * (g >> 1);
-                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4 *)(ldsV + kvoff(kb + qq, chk) + 8 * (pp & 1)));
-                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4 *)(ldsV + kvoff(kb + 8 + qq, chk) + 8 * (pp & 1)));
-                    // whole-vector reinterpretation (per-element bit_cast<__bf16> insertion
-                    // is miscompiled by ROCm 7.2 hipcc: it keeps only the first dword)
-                    const s16x8 cat = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                    const bf16x8 vf = __builtin_bit_cast(bf16x8, cat);
-                    oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
-                }
-        }
+        const uint32_t vb = lds_base + (uint32_t)(ldsV - lds);
+        s16x4 ra[2][2][2], rb[2][2][2];
+        pv_reads(vb, 0, ra);
+        pv_wait(ra);
+        pv_reads(vb, 1, rb);
+        pv_mfma(0, ra, pf);
+        pv_wait(rb);
+        pv_reads(vb, 2, ra);
+        pv_mfma(1, rb, pf);
+        pv_wait(ra);
+        pv_reads(vb, 3, rb);
+        pv_mfma(2, ra, pf);
+        pv_wait(rb);
+        pv_mfma(3, rb, pf);
     };
 
-    if (ntiles > 0) stage_tile(t_first * KT, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // end-of-tile wait: own DMAs of the NEXT tile landed (ring3: the one after stays in
+    // flight — vmcnt counts this wave's GPW LDS-DMAs of it), then the barrier publishes
+    // them to every wave and retires this tile's reads (WAR for the refill two tiles on)
+    // (a raw s_barrier: __syncthreads() would add a full vmcnt(0) drain)
+    auto tile_barrier = [&](bool two_ahead) {
+        if (ATT_RING3 && two_ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
+
+    if (ntiles > 0) stage_tile(t_first * KT, 0);
+    if (ATT_RING3 && ntiles > 1) stage_tile((t_first + 1) * KT, 1);
+    tile_barrier(ntiles > 1);
     for (int it = 0; it < ntiles; ++it) {
         const int kv0 = (t_first + it) * KT;
         const int cur = it % NBUF;
-        const bool more = it + 1 < ntiles;
-        if (more) stage_tile(kv0 + KT, (it + 1) % NBUF);   // tile it−2's slot: read by nobody now
+        if (ATT_RING3) {
+            if (it + 2 < ntiles) stage_tile(kv0 + 2 * KT, (it + 2) % NBUF);   // tile it−1's slot: retired
+        } else if (it + 1 < ntiles) {
+            stage_tile(kv0 + KT, (it + 1) % NBUF);          // tile it−2's slot: read by nobody now
+        }
         const char *ldsK = lds + cur * 2 * TILE;
         const char *ldsV = ldsK + TILE;
         // deferred half: the previous tile's P·V first (O is still at that tile's max)
@@ -210,22 +313,29 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                               (causal ? kv0 + KT - 1 <= q0
                                       : (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window)));
         if (outside && !defer) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+            tile_barrier(it + 2 < ntiles);
             continue;
         }
 
         // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
+        // K fragments by asm reads (see pv()); the reads of key half t=1 are in flight
+        // during the MFMAs of t=0
         f32x16 st[2];
+        {
+            const uint32_t kbase = lds_base + cur * 2 * TILE;
+            bf16x8 k0[8], k1[8];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+            for (int s = 0; s < 8; ++s) k0[s] = ds_read_b128_at(koff[s], kbase);
+            lgkm_wait8(k0);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
+            for (int s = 0; s < 8; ++s) k1[s] = ds_read_b128_at(koff[s], kbase + 32 * 256);
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const bf16x8 kf = *(const bf16x8 *)(ldsK + kvoff(32 * t + r, 2 * s + hh));
-                st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
-            }
+            for (int j = 0; j < 16; ++j) { st[0][j] = 0.f; st[1][j] = 0.f; }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[s], qf[s], st[0], 0, 0, 0);
+            lgkm_wait8(k1);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[s], qf[s], st[1], 0, 0, 0);
         }
         // running max on raw scores (scale folded into the exp2 FMA below);
         // interior tiles of full / cross attention need no mask
@@ -255,7 +365,10 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                 }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-        const float mn = fmaxf(m, mx);
+        // lazy rescale: the running reference max moves only when a score exceeds it by more
+        // than ATT_TAU (log2 units), so P = 2^(s − m) ≤ 2^TAU and after the first tiles the
+        // O/l rescale (64 VALU per lane) is skipped almost always; O/l is the same softmax
+        const float mn = mx > m + ATT_TAU ? mx : m;
         const float alpha = __builtin_amdgcn_exp2f(m - mn);   // raw v_exp_f32 (no denormal range fix-up)
         m = mn;
         float rs = 0.f;
@@ -284,8 +397,7 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
 #pragma unroll
                 for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
         if (!defer) pv(ldsV, pf);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own DMA landed; the barrier publishes it
-        __syncthreads();
+        tile_barrier(it + 2 < ntiles);
     }
     if (defer && ntiles > 0) pv(lds + ((ntiles - 1) % NBUF) * 2 * TILE + TILE, pf);
 
