@@ -32,6 +32,15 @@ namespace {
 
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
+#ifndef W4_DMA_EVERY
+#define W4_DMA_EVERY 0     // 4-wave GEMM refill spacing in MFMAs (0: spread over half B)
+#endif
+#ifndef W4_DMA_FIRST
+#define W4_DMA_FIRST 1     // MFMA index of the first refill piece (−1: all before the reads)
+#endif
+#ifndef W4_COST
+#define W4_COST 0.92       // 4-wave 192×256 tile time relative to the ping-pong one (cost model)
+#endif
 #ifndef PP_SCHED
 #define PP_SCHED -1        // ping-pong main loop: -1 per tile (256 rows: 1, 192 rows: 0); 0 12/4/8/0-read phases, 1 8/4/8/4, 2 two phases
 #endif
@@ -80,35 +89,67 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                 const int nout = ((col0 + pnl * 64) >> 1) + (odd ? 16 : 0) + cpos;
                 if (live) *(uint4 *)(a.C + (int64_t)m * a.ldc + nout) = pack8(o);
             }
-        } else {
-            const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
+        }
+    }
+    if constexpr (EPI != EPI_SWIGLU) {
+        // operand loads (residual, gate, bias) of a chunk of CH row groups are all issued
+        // before its first store: the stores may alias them (in-place residual: C == res),
+        // so the compiler would otherwise wait for every load right after issuing it —
+        // one full memory latency per 16-B store, exposed at one wave per SIMD
+        constexpr int NP = SN / 2, CH = (12 / NP) < 1 ? 1 : (12 / NP);
 #pragma unroll
-            for (int jp = 0; jp < SN / 2; ++jp) {
-                float o[8];
-                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
-                const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                if (!live) continue;
-                if constexpr (EPI == EPI_STORE) {
-                    if (a.bias) {
-                        float bb[8];
-                        unpack8(*(const uint4 *)(a.bias + n), bb);
+        for (int c0 = 0; c0 < SM; c0 += CH) {
+            uint4 rv[CH][NP], gv[CH][NP];
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) o[r] += bb[r];
-                    }
-                } else {
-                    float rr[8];
-                    unpack8(*(const uint4 *)(a.res + (int64_t)m * a.ldr + n), rr);
-                    if constexpr (EPI == EPI_GATED_RES) {
-                        float gg[8];
-                        unpack8(*(const uint4 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n), gg);
+            for (int ii = 0; ii < CH; ++ii) {
+                if (c0 + ii >= SM) break;
+                const int m = min(row0 + (c0 + ii) * 16 + fr, a.M - 1);
+                const int bb_ = (EPI == EPI_GATED_RES) ? m / a.rows_per_batch : 0;
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(rbf(o[r]) * gg[r]);
+                for (int jp = 0; jp < NP; ++jp) {
+                    const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
+                    if constexpr (EPI == EPI_STORE) {
+                        if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n);
                     } else {
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(o[r]);
+                        rv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
+                        if constexpr (EPI == EPI_GATED_RES)
+                            gv[ii][jp] = *(const uint4 *)(a.gate + (int64_t)bb_ * a.gate_bstride + n);
                     }
                 }
-                *(uint4 *)(a.C + (int64_t)m * a.ldc + n) = pack8(o);
+            }
+#pragma unroll
+            for (int ii = 0; ii < CH; ++ii) {
+                if (c0 + ii >= SM) break;
+                const int i = c0 + ii;
+                const int m = row0 + i * 16 + fr;
+                const bool live = m < a.M;       // rows past M still join the lane exchange
+#pragma unroll
+                for (int jp = 0; jp < NP; ++jp) {
+                    float o[8];
+                    pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                    const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
+                    if constexpr (EPI == EPI_STORE) {
+                        if (a.bias) {
+                            float bb[8];
+                            unpack8(rv[ii][jp], bb);
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                        }
+                    } else {
+                        float rr[8];
+                        unpack8(rv[ii][jp], rr);
+                        if constexpr (EPI == EPI_GATED_RES) {
+                            float gg[8];
+                            unpack8(gv[ii][jp], gg);
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(rbf(o[r]) * gg[r]);
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(o[r]);
+                        }
+                    }
+                    if (live) *(uint4 *)(a.C + (int64_t)m * a.ldc + n) = pack8(o);
+                }
             }
         }
     }
@@ -250,6 +291,66 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a, int sp
         }
     }
     *(uint2 *)(out + (int64_t)m * ldo + q) = pack4(o);
+}
+
+// Head-post epilogue of a BM×256 QKV tile (two 128-column heads): bf16(acc) → LDS tile
+// [BM][PITCH] (the operand ring is dead; store_acc(st, PITCH) writes the wave's
+// accumulators), then one 16-lane group per (row, head): RMSNorm + RoPE + head-major
+// store.  A lane's units: a fixed head (hh = sub & 1) and rows r = wave·2 + (sub >> 1)
+// + 2·NW·it, so (batch, position) advance incrementally (no integer division per unit)
+// and every cos/sin row is loaded BEFORE the first store (a load's vmcnt would
+// otherwise also wait for the older stores).
+template <int BM, int NW, int LDS_BYTES, typename StoreAcc>
+__device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, int m0, int n0, int wave, int lane,
+                                                  StoreAcc store_acc) {
+    constexpr int PITCH = 264;   // 528-B rows: 16-B aligned, 2-way conflicts on the 8-B writes
+    constexpr int RPI = 2 * NW;  // rows per iteration
+    constexpr int ITER = BM / RPI;
+    static_assert(BM % RPI == 0, "rows must split evenly over the iterations");
+    static_assert(BM * PITCH * 2 <= LDS_BYTES, "head-post staging tile must fit the operand ring");
+    const HeadPostArgs &h = a.hp;
+    const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = sub & 1;
+    const int head = (n0 >> 7) + hh;
+    const bool norm = head < h.nq + h.nk;
+    const bool rope = h.cos != nullptr;
+    const int r0 = wave * 2 + (sub >> 1);
+    const int mf = min(m0 + r0, a.M - 1);
+    const int b0 = mf / h.S, s0 = mf - b0 * h.S;
+    uint4 cv[ITER], sv[ITER];
+    if (rope) {
+        int sq = s0;
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+            const int sc = min(sq, h.S - 1);
+            cv[it] = *(const uint4 *)(h.cos + (int64_t)sc * 128 + d);
+            sv[it] = *(const uint4 *)(h.sin + (int64_t)sc * 128 + d);
+            sq += RPI;
+            while (sq >= h.S) sq -= h.S;
+        }
+    }
+    float w[8] = {};
+    if (norm) unpack8(*(const uint4 *)((head < h.nq ? h.qw : h.kw) + d), w);
+    bf16_t *st = (bf16_t *)lds;
+    __syncthreads();
+    store_acc(st, PITCH);
+    __syncthreads();
+    int bq = b0, sq = s0;
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int r = r0 + RPI * it;
+        float x[8], cs[8] = {}, sn[8] = {};
+        unpack8(*(const uint4 *)(st + r * PITCH + hh * 128 + d), x);
+        if (rope) {
+            unpack8(cv[it], cs);
+            unpack8(sv[it], sn);
+        }
+        const bf16_t *nw;
+        bf16_t *dst = head_dst(h, head, bq, sq, nw);
+        head_norm_rope(x, li, norm, w, rope, cs, sn, h.eps);
+        if (m0 + r < a.M && dst) *(uint4 *)(dst + d) = pack8(x);
+        sq += RPI;
+        while (sq >= h.S) { sq -= h.S; ++bq; }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -506,68 +607,182 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     if (wr == 0) bar();   // balance the barrier count
 
     if constexpr (EPI == EPI_HEADPOST) {
-        // bf16(acc) → LDS tile [BM][PITCH] (the operand ring is dead), then one 16-lane group
-        // per (row, 128-column head): RMSNorm + RoPE + head-major store.  A lane's units are
-        // uu = wave·4 + 32·it + sub: a fixed head (hh = sub & 1) and rows
-        // r = wave·2 + (sub >> 1) + 16·it, so (batch, position) advance incrementally (no
-        // integer division per unit) and every cos/sin row is loaded BEFORE the first store
-        // (a load's vmcnt would otherwise also wait for the older stores).
-        constexpr int PITCH = 264;   // 528-B rows: 16-B aligned, 2-way conflicts on the 8-B writes
-        constexpr int ITER = BM * 2 / 32;
-        static_assert(BM * PITCH * 2 <= 2 * BUF, "head-post staging tile must fit the operand ring");
-        const HeadPostArgs &h = a.hp;
-        const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = sub & 1;
-        const int head = (n0 >> 7) + hh;
-        const bool norm = head < h.nq + h.nk;
-        const bool rope = h.cos != nullptr;
-        const int r0 = wave * 2 + (sub >> 1);
-        const int mf = min(m0 + r0, a.M - 1);
-        const int b0 = mf / h.S, s0 = mf - b0 * h.S;
-        uint4 cv[ITER], sv[ITER];
-        if (rope) {
-            int sq = s0;
+        headpost_epilogue<BM, 8, sizeof(lds)>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
-            for (int it = 0; it < ITER; ++it) {
-                const int sc = min(sq, h.S - 1);
-                cv[it] = *(const uint4 *)(h.cos + (int64_t)sc * 128 + d);
-                sv[it] = *(const uint4 *)(h.sin + (int64_t)sc * 128 + d);
-                sq += 16;
-                while (sq >= h.S) sq -= h.S;
-            }
-        }
-        float w[8] = {};
-        if (norm) unpack8(*(const uint4 *)((head < h.nq ? h.qw : h.kw) + d), w);
-        bf16_t *st = (bf16_t *)lds;
-        __syncthreads();
+            for (int i = 0; i < SM; ++i)
 #pragma unroll
-        for (int i = 0; i < SM; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-                *(uint2 *)(st + (arow + i * 16 + fr) * PITCH + wc * 64 + j * 16 + fc * 4) = pack4(o);
-            }
-        __syncthreads();
-        int bq = b0, sq = s0;
-#pragma unroll
-        for (int it = 0; it < ITER; ++it) {
-            const int r = r0 + 16 * it;
-            float x[8], cs[8] = {}, sn[8] = {};
-            unpack8(*(const uint4 *)(st + r * PITCH + hh * 128 + d), x);
-            if (rope) {
-                unpack8(cv[it], cs);
-                unpack8(sv[it], sn);
-            }
-            const bf16_t *nw;
-            bf16_t *dst = head_dst(h, head, bq, sq, nw);
-            head_norm_rope(x, li, norm, w, rope, cs, sn, h.eps);
-            if (m0 + r < a.M && dst) *(uint4 *)(dst + d) = pack8(x);
-            sq += 16;
-            while (sq >= h.S) { sq -= h.S; ++bq; }
-        }
+                for (int j = 0; j < 4; ++j) {
+                    float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                    *(uint2 *)(st + (arow + i * 16 + fr) * pitch + wc * 64 + j * 16 + fc * 4) = pack4(o);
+                }
+        });
         return;
     }
 
     epilogue_tile<SM, 4, EPI>(a, acc, m0 + arow, n0 + wc * 64, fr, fc);
+}
+
+// ---------------------------------------------------------------------------
+// Four-wave variant: BM×256 tile, one wave per SIMD (2×2 waves, wave tile
+// (BM/2)×128: 48 or 64 accumulators of 16×16, in AGPRs), register double-buffered
+// fragments.  Per K-tile kt (two 32-deep k-steps), ONE barrier in the middle:
+//   half A   MFMAs of k-step 0 (fragments F0)  ∥ ds_reads of k-step 1 → F1
+//   ──────   own LDS-DMA of tile kt+1 retired (vmcnt(0): nothing newer is in
+//            flight yet) + own reads retired, barrier: tile kt+1 is visible and
+//            every wave has finished reading tile kt
+//   half B   LDS-DMA of tile kt+2 into tile kt's buffer, MFMAs of k-step 1 (F1)
+//            ∥ ds_reads of tile kt+1's k-step 0 → F0
+// so the MFMA pipe never waits for a fragment read, the DMA of a tile has one whole
+// K-tile (≈96 MFMAs) of lead, and two LDS buffers suffice.
+template <int BM, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
+    constexpr int BN = 256, TM = BM / 2, TN = 128, SM = TM / 16, SN = TN / 16;
+    constexpr int ROWS = BM + BN, STAGE = ROWS * 128;
+    constexpr int PW = ROWS / 32;                              // glds per wave per K-tile
+    static_assert(ROWS % 32 == 0, "staging must split evenly over 4 waves");
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
+    const int nwg = tilesM * tilesN;
+    const int wg = xcd_remap(blockIdx.x, nwg);
+    const int per_group = GROUP_M * tilesN;
+    const int gid = wg / per_group, first_m = gid * GROUP_M;
+    const int gsz = min(tilesM - first_m, GROUP_M);
+    const int tm = first_m + (wg % per_group) % gsz;
+    const int tn = (wg % per_group) / gsz;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // staging: wave issues image rows [8q, 8q+8) for q = wave + 4i (swizzle on the source)
+    const bf16_t *src[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int r = (wave + 4 * i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        if (r < BM) src[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8;
+        else src[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8;
+    }
+    auto stage1 = [&](int buf, int k0, int i) { glds16(src[i] + k0, lds + buf * STAGE + (wave + 4 * i) * 1024); };
+
+    f32x4 acc[SM][SN];
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fc = lane >> 4;
+    const int xrow = wm * TM + fr, wrow = BM + wn * TN + fr;
+    bf16x8 x0[SM], w0[SN], x1[SM], w1[SN];
+    auto rd = [&](const char *b, int ks, bf16x8 (&xf)[SM], bf16x8 (&wf)[SN]) {
+#pragma unroll
+        for (int j = 0; j < SN; ++j) wf[j] = *(const bf16x8 *)(b + swz(wrow + j * 16, ks * 4 + fc));
+#pragma unroll
+        for (int i = 0; i < SM; ++i) xf[i] = *(const bf16x8 *)(b + swz(xrow + i * 16, ks * 4 + fc));
+    };
+    // MFMA by inline asm with the accumulator tied in place in AGPRs ("+a"): with the
+    // builtin, the register allocator of ROCm 7.2 splits dst from srcC at this register
+    // pressure (192 accumulators + 112 fragment registers) and rotates the whole
+    // accumulator set through v_accvgpr_mov copies every K-tile
+    // hook(n) runs after the n-th MFMA (the LDS-DMA pieces of a refill are spread over
+    // the MFMA stream this way: volatile asm and the DMA builtin keep their order)
+    auto mm = [&](const bf16x8 (&xf)[SM], const bf16x8 (&wf)[SN], auto hook) {
+#pragma unroll
+        for (int i = 0; i < SM; ++i)
+#pragma unroll
+            for (int j = 0; j < SN; ++j) {
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wf[j]), "v"(xf[i]));
+                hook(i * SN + j);
+            }
+    };
+    auto none = [](int) {};
+    // the wait is the builtin (vmcnt(0) expcnt(7) lgkmcnt(0)), so the compiler's own
+    // waitcnt pass knows every read before it has retired and adds none after it
+    auto bar = [] {
+        __builtin_amdgcn_s_waitcnt(0x0070);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // (F0 was read during the previous half B: retire it with a compiler-visible
+    // lgkmcnt(0) — vmcnt(63) expcnt(7) — before the next reads are issued, or the
+    // compiler waits lgkmcnt(0) for it behind them)
+    //
+    // ONE straight-line loop body for every K-tile, the last ones included: the refill
+    // source is clamped to the last tile (a duplicate load into a buffer nobody reads
+    // again) and the last iteration's "next" reads hit a stale buffer (unused).  A
+    // second copy of the MFMA code (a peeled tail) makes the register allocator move the
+    // accumulators between copies with VALU instructions that the asm MFMAs — opaque
+    // to the hazard recognizer — would read without the required wait states.
+    const int nk = a.K / BK;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) stage1(0, 0, i);
+    if (nk > 1) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) stage1(1, BK, i);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd(lds, 0, x0, w0);
+    // refill pieces: one after every EVERY-th MFMA of half B, from MFMA FIRST on
+    constexpr int EVERY = W4_DMA_EVERY > 0 ? W4_DMA_EVERY : SM * SN / PW, FIRST = W4_DMA_FIRST;
+    static_assert(FIRST + EVERY * (PW - 1) < SM * SN, "refill pieces must fit in half B");
+    for (int kt = 0; kt < nk; ++kt) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        rd(lds + (kt & 1) * STAGE, 1, x1, w1);
+        mm(x0, w0, none);
+        bar();
+        const int kr = min(kt + 2, nk - 1) * BK;
+        if constexpr (FIRST < 0) {
+#pragma unroll
+            for (int i = 0; i < PW; ++i) stage1(kt & 1, kr, i);
+        }
+        rd(lds + ((kt + 1) & 1) * STAGE, 0, x0, w0);
+        mm(x1, w1, [&](int n) {
+            if (FIRST >= 0 && n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW)
+                stage1(kt & 1, kr, (n - FIRST) / EVERY);
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the asm MFMAs are opaque to the hazard recognizer: let the last ones retire
+    // before their accumulators are read
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+    if constexpr (EPI == EPI_HEADPOST) {
+        headpost_epilogue<BM, 4, sizeof(lds)>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
+#pragma unroll
+            for (int i = 0; i < SM; ++i)
+#pragma unroll
+                for (int j = 0; j < SN; ++j) {
+                    float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                    *(uint2 *)(st + (wm * TM + i * 16 + fr) * pitch + wn * TN + j * 16 + fc * 4) = pack4(o);
+                }
+        });
+    } else {
+        epilogue_tile<SM, SN, EPI>(a, acc, m0 + wm * TM, n0 + wn * TN, fr, fc);
+    }
+}
+
+template <int BM>
+int launch_w4(const GemmArgs &a, hipStream_t s) {
+    if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
+    const int tiles = ((a.M + BM - 1) / BM) * (a.N / 256);
+    switch (a.epi) {
+        case EPI_STORE: gemm_w4_kernel<BM, EPI_STORE><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_w4_kernel<BM, EPI_GATED_RES><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_RES: gemm_w4_kernel<BM, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_SWIGLU: gemm_w4_kernel<BM, EPI_SWIGLU><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_HEADPOST:
+            if constexpr (BM == 192) {
+                gemm_w4_kernel<BM, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
+                break;
+            }
+            return fail(-1, "gemm: the head-post epilogue needs the 192-row tile");
+        default: return fail(-1, "gemm: bad epilogue for the 4-wave variant");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 template <int BM>
@@ -622,6 +837,7 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 8: return launch_pp<192>(a, s);              // ping-pong 192x256 (112 KiB)
         case 9: return launch<192, 256, 2, 2, 2>(a, s);   // 4 waves (1/SIMD), 96x128 wave tile, acc in AGPRs
         case 10: return launch<256, 256, 2, 2, 2>(a, s);  // 4 waves (1/SIMD), 128x128 wave tile
+        case 11: return launch_w4<192>(a, s);             // 4 waves, 96x128 wave tile, pipelined fragments
         default: return fail(-1, "gemm: bad variant");
     }
 }
@@ -646,12 +862,26 @@ static int num_cus() {
 // model reproduces the measured v7/v8 ratios on all four DiT shapes to 2 %.
 // Grids that fill at most half the chip fall back to 128×128 (2 blocks/CU): at
 // M = 3000, N = 2048 (the cross-O GEMM of the conditional rows) 37 µs vs 46 µs.
+// ACEHIP_GEMM_W4=1 runs the 192×256 tile as the four-wave pipelined kernel (variant 11)
+// instead of the ping-pong one.  In isolation (store epilogue) it is 0.92–0.98× the
+// ping-pong time; inside the DiT (cold weights, residual / head-post epilogues at one
+// wave per SIMD) it is 1.05–1.17× (r02 A/B: 0.581 vs 0.562 s/song), so it is off.
+static bool use_w4() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_GEMM_W4");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 int gemm_pick_variant(int64_t M, int N) {
     if (N % 256) return 0;
     const int cus = num_cus();
     const int64_t t7 = ((M + 255) / 256) * (N / 256), t8 = ((M + 191) / 192) * (N / 256);
     if (t8 <= cus / 2) return 0;
     const double c7 = (double)((t7 + cus - 1) / cus) * 1.093, c8 = (double)((t8 + cus - 1) / cus);
+    if (use_w4()) return c7 < c8 * W4_COST ? 7 : 11;
     return c7 < c8 ? 7 : 8;
 }
 
@@ -712,7 +942,7 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     if (a.epi != EPI_SWIGLU && a.epi != EPI_STORE) return 1;
     const char *e = getenv("ACEHIP_GEMM_TAILSPLIT");
     if (e && e[0] == '0') return 1;
-    const int BMv = v == 7 ? 256 : 192, cus = num_cus();
+    const int BMv = v == 7 ? 256 : 192, cus = num_cus();   // v = 7, 8 or 11
     const int64_t nN = a.N / 256, tiles = (int64_t)((a.M + BMv - 1) / BMv) * nN;
     const int64_t full = tiles / cus, rem = tiles - full * cus;
     if (full < 1 || rem == 0 || rem * 5 > (int64_t)cus * 3) return 1;   // last round > 60 % full
@@ -774,17 +1004,17 @@ int gemm(const GemmArgs &a, hipStream_t s) {
             hh.ld_src = a.N;
             return head_post(hh, s);
         }
-        return launch_pp<192>(a, s);
+        return use_w4() ? launch_w4<192>(a, s) : launch_pp<192>(a, s);
     }
     int v = g_variant_override;
     if (v < 0) {
         v = gemm_pick_variant(a.M, a.N);
-        if (v == 7 || v == 8) {
+        if (v == 7 || v == 8 || v == 11) {
             const int rc = gemm_tail_split(a, v, s);
             if (rc <= 0) return rc;   // split done (0) or failed (< 0); 1 = not applicable
         }
     }
-    if ((v == 3 || v >= 5) && a.N % 256) v = 0;
+    if ((v == 3 || v >= 5) && a.N % 256) v = 0;   // (11, 12 too)
     return gemm_variant(a, v, s);
 }
 

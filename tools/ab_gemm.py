@@ -34,6 +34,11 @@ def load(path):
 
 
 libs = [load(None)] + [load(p) for p in sys.argv[1:]]
+# AB_VARIANT forces one variant for every shape (A/B of a kernel's schedule builds)
+if os.environ.get("AB_VARIANT"):
+    SHAPES = {k: v[:4] + (int(os.environ["AB_VARIANT"]),) for k, v in SHAPES.items()}
+if os.environ.get("SHAPES"):
+    SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 res = {}
 for name, (M, N, K, epi, var) in SHAPES.items():
     g = torch.Generator(device=dev).manual_seed(0)
@@ -72,8 +77,22 @@ for name, (M, N, K, epi, var) in SHAPES.items():
             e1.record()
             torch.cuda.synchronize()
             times[ln].append(e0.elapsed_time(e1) / n * 1e3)
+    # hipBLASLt (torch.matmul, plain store, no epilogue) on the same box for reference
+    Wts = [w.t() for w in Ws]
+    for i in range(3):
+        torch.matmul(A, Wts[i % nrot])
+    tt = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(20):
+            torch.matmul(A, Wts[i % nrot])
+        e1.record()
+        torch.cuda.synchronize()
+        tt.append(e0.elapsed_time(e1) / 20 * 1e3)
     fl = 2.0 * M * N * K
-    row = {}
+    row = {"torch(hipBLASLt)": {"us": round(statistics.median(tt), 1),
+                                "tflops": round(fl / statistics.median(tt) * 1e-6, 1)}}
     for ln in times:
         us = statistics.median(times[ln])
         d = float((outs[ln] - outs["tree"]).abs().max())

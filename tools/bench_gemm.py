@@ -29,7 +29,7 @@ for name, (M, N, K) in shapes.items():
     fl = 2.0 * M * N * K
     row = {}
     for v in variants:
-        if v in (3, 5, 6, 7, 8, 9, 10) and N % 256:
+        if v in (3, 5, 6, 7, 8, 9, 10, 11) and N % 256:
             continue
         def run():
             Wr = Ws[rot[0] % nrot]

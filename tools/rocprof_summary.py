@@ -5,10 +5,13 @@ calls, total ms, average µs and share — the table ``--stats`` prints.
 
 usage: rocprof_summary.py results.db [--by-name]
 """
+import os
 import re
 import sqlite3
 import sys
 from collections import defaultdict
+
+NAMEW = int(os.environ.get("NAMEW", "120"))
 
 
 def _short(name: str) -> str:
@@ -33,7 +36,7 @@ def summarize(db_path, top=45, by_name=False):
     rows = sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]
     lines = ["| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
     for k, (n, ms) in rows:
-        lines.append(f"| `{k[:120]}` | {n} | {ms:.2f} | {ms / n * 1e3:.1f} | {100 * ms / total:.1f} |")
+        lines.append(f"| `{k[:NAMEW]}` | {n} | {ms:.2f} | {ms / n * 1e3:.1f} | {100 * ms / total:.1f} |")
     lines.append(f"| **total** | {sum(v[0] for v in agg.values())} | {total:.2f} | | 100 |")
     return "\n".join(lines)
 
