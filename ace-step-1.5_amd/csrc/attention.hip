@@ -39,22 +39,21 @@
 namespace acehip {
 namespace {
 
-#ifndef ATT_DEFER
-#define ATT_DEFER 0        // second head's waves run P·V one tile late (SIMD-partner stagger;
-#endif                     // measured neutral-to-negative on MI355X, kept as an A/B switch)
 #ifndef ATT_XCD
 #define ATT_XCD 1          // XCD-aware block → work-unit remap
 #endif
 #ifndef ATT_PRIO
-#define ATT_PRIO 1         // static s_setprio 1 for the deferred (younger) half
+#define ATT_PRIO 1         // static s_setprio 1 for the younger half (waves 4-7)
 #endif
 #ifndef ATT_TAU
 #define ATT_TAU 8.0f       // lazy-rescale threshold (0: rescale on every new max)
 #endif
-#ifndef ATT_RING3
-#define ATT_RING3 0        // 3-deep K/V ring: tile j+2 in flight behind a counted vmcnt across the
-#endif                     // barrier (the 2-deep ring drained the DMA queue with vmcnt(0) every tile)
-static_assert(!(ATT_DEFER && ATT_RING3), "the deferred P·V reads V(j-1), which the 3-deep ring refills");
+#ifndef ATT_RING_BAND
+#define ATT_RING_BAND 2    // K/V ring depth (tiles) of band layers: D−1 tiles in flight behind a
+#endif                     // counted vmcnt (r02 A/B at 240 s: depth 2 53.7 µs, 3 56.3, 4 56.2)
+#ifndef ATT_RING_FULL
+#define ATT_RING_FULL 2    // full / cross / causal / key-masked: one tile ahead (L2-warm K/V)
+#endif
 
 constexpr int QB = 128;    // queries per workgroup
 constexpr int KT = 64;     // keys per tile
@@ -119,7 +118,7 @@ __device__ __forceinline__ int kvoff(int row, int ch) {
 // NREP = query heads per KV head handled by one workgroup (GQA sharing:
 // each K/V tile is staged once for all NREP heads).  4 waves × 32 queries
 // per head → QB = 128 queries per head per workgroup.
-template <int NREP>
+template <int NREP, int D>
 __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *__restrict__ q,
                                                                   const bf16_t *__restrict__ k,
                                                                   const bf16_t *__restrict__ v,
@@ -129,7 +128,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const uint8_t *__restrict__ kmask) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
-    constexpr int NBUF = (ATT_DEFER || ATT_RING3) ? 3 : 2;   // K/V ring (deferred P·V still reads V(j−1))
+    constexpr int NBUF = D;                        // K/V ring slots (tiles)
+    static_assert(D >= 2 && D <= 4, "ring depth");
     constexpr int GPW = 32 / (NT / 64);            // LDS-DMA instructions per wave per tile
     __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -152,11 +152,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const int qblk = qb * QB;
     const int q0 = qblk + (wave & 3) * 32;
     const int qi = q0 + r;
-    // SIMD partners (wave w and w+4) are staggered: the second half defers each
-    // tile's P·V into the next iteration, so one partner's softmax (VALU) runs
-    // beside the other's MFMAs; the younger half gets static priority
-    // (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
-    const bool defer = ATT_DEFER && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4;
+    // the younger half of the SIMD partners (waves 4-7) gets static priority
+    // (MI355X_MICROARCH.md "Two waves per SIMD", item 4)
     if (ATT_PRIO && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[qi][16s + 8hh .. +8]
@@ -278,33 +275,33 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         pv_mfma(3, rb, pf);
     };
 
-    // end-of-tile wait: own DMAs of the NEXT tile landed (ring3: the one after stays in
-    // flight — vmcnt counts this wave's GPW LDS-DMAs of it), then the barrier publishes
-    // them to every wave and retires this tile's reads (WAR for the refill two tiles on)
-    // (a raw s_barrier: __syncthreads() would add a full vmcnt(0) drain)
-    auto tile_barrier = [&](bool two_ahead) {
-        if (ATT_RING3 && two_ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GPW) : "memory");
+    // wait until tile `need` landed: own DMAs retired down to the `newer` tiles staged
+    // after it (vmcnt counts this wave's GPW LDS-DMAs per tile), own LDS reads retired;
+    // then the barrier publishes the tile to every wave and retires the current tile's
+    // reads (WAR for the refill of its slot) — a raw s_barrier: __syncthreads() would
+    // add a full vmcnt(0) drain
+    auto tile_barrier = [&](int newer) {
+        if (D >= 4 && newer >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GPW) : "memory");
+        else if (D >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GPW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
 
-    if (ntiles > 0) stage_tile(t_first * KT, 0);
-    if (ATT_RING3 && ntiles > 1) stage_tile((t_first + 1) * KT, 1);
-    tile_barrier(ntiles > 1);
+    // ring of D slots: tiles 0..D−2 staged up front; iteration it stages tile it+D−1 into
+    // the slot of tile it−1 (its last reads retired before the barrier that ended
+    // iteration it−1) and ends waiting for tile it+1 with min(D−2, …) newer tiles in flight
+#pragma unroll
+    for (int t = 0; t < D - 1; ++t)
+        if (t < ntiles) stage_tile((t_first + t) * KT, t);
+    tile_barrier(min(D - 2, ntiles - 1));
     for (int it = 0; it < ntiles; ++it) {
         const int kv0 = (t_first + it) * KT;
         const int cur = it % NBUF;
-        if (ATT_RING3) {
-            if (it + 2 < ntiles) stage_tile(kv0 + 2 * KT, (it + 2) % NBUF);   // tile it−1's slot: retired
-        } else if (it + 1 < ntiles) {
-            stage_tile(kv0 + KT, (it + 1) % NBUF);          // tile it−2's slot: read by nobody now
-        }
+        if (it + D - 1 < ntiles) stage_tile(kv0 + (D - 1) * KT, (it + D - 1) % NBUF);
         const char *ldsK = lds + cur * 2 * TILE;
         const char *ldsV = ldsK + TILE;
-        // deferred half: the previous tile's P·V first (O is still at that tile's max)
-        if (defer && it > 0) pv(lds + ((it + NBUF - 1) % NBUF) * 2 * TILE + TILE, pf);
         // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
         // skipped (the wave still joins the barrier); one entirely inside needs no mask
         const bool outside = (window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window)) ||
@@ -312,8 +309,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         const bool interior = !km && kv0 + KT <= Sk &&
                               (causal ? kv0 + KT - 1 <= q0
                                       : (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window)));
-        if (outside && !defer) {
-            tile_barrier(it + 2 < ntiles);
+        if (outside) {
+            tile_barrier(min(D - 2, ntiles - 2 - it));
             continue;
         }
 
@@ -396,10 +393,9 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
             for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
-        if (!defer) pv(ldsV, pf);
-        tile_barrier(it + 2 < ntiles);
+        pv(ldsV, pf);
+        tile_barrier(min(D - 2, ntiles - 2 - it));
     }
-    if (defer && ntiles > 0) pv(lds + ((ntiles - 1) % NBUF) * 2 * TILE + TILE, pf);
 
     if (nsplit > 1) {
         // publish this part's (O, m, l) in lane order, then take a ticket; the last
@@ -521,10 +517,13 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
     }
     const int grid = sp.full + (units - sp.full) * sp.nsplit;
-    if (nrep == 2) {
-        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
+    const bool band = window >= 0 && !kmask;
+    if (nrep == 2 && band) {
+        attn_fwd_kernel<2, ATT_RING_BAND><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
+    } else if (nrep == 2) {
+        attn_fwd_kernel<2, ATT_RING_FULL><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else if (nrep == 1) {
-        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
+        attn_fwd_kernel<1, 2><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else {
         return fail(-1, "attention: heads/kv_heads must be 1 or 2");
     }
