@@ -302,6 +302,246 @@ __global__ __launch_bounds__(256, 2) void resunit128_kernel(ResUnitArgs u) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k=7 dilated stride-1 convolution with the INPUT WINDOW staged once per channel
+// chunk instead of an im2col tile per tap (conv_gemm_kernel fetches every input row
+// 7× through L2 and waits vmcnt(0) on a one-tile ring every K-tile).
+// Tile 256 positions × 128 output channels, 8 waves (4 M × 2 N, 64×64 wave tiles).
+// K loop: kt = cc·7 + tap over 64-channel chunks cc; per K-tile the A fragments
+// come from the window image of chunk cc (row = position − m0 + 3·dil + tap·dil −
+// 3·dil), the W tile (128 rows × 64 k) from a 3-slot ring.  One barrier per K-tile:
+//   top of kt   own DMAs of W(kt) (and, older, window(cc)) retired — counted vmcnt,
+//               newer W(kt+1) / window(cc+1) stay in flight — then the barrier
+//   after it    stage W(kt+2) into slot (kt+2)%3 (tile kt−1's, read before the
+//               barrier), and at tap 0 window(cc+1) into the other window buffer
+//               (chunk cc−1's, last read at K-tile kt−1).
+// Window image: 128-B rows (64 channels), physical chunk = chunk ^ (row & 7), which
+// keeps every ds_read_b128 lane group conflict-free for ANY row offset (the tap
+// shift tap·dil misaligns the fragment rows; tools/conv_swizzle check, r02).
+// FUSED (C = 128): the residual unit — y_s = snake2(conv7 + b1) into LDS, then the
+// k=1 GEMM with W2 and x' = x + (W2·y_s + b2), snaked for the next unit.
+// Two geometries: BM = 256 / 8 waves / 3 W slots (128 KiB LDS, one block per CU) and
+// BM = 128 / 4 waves / 2 W slots (80 KiB: two blocks per CU, whose epilogues and main
+// loops interleave — the epilogue VALU (bias, bf16 rounding, Snake) is ≈ the MFMA time)
+template <int BM_>
+struct Conv7 {
+    static constexpr int BM = BM_, BN = 128, NW = BM / 32;
+    static constexpr int WSLOTS = BM == 256 ? 3 : 2;
+    static constexpr int WROWS = BM == 256 ? 320 : 192;      // window rows ≥ BM + 6·9
+    static constexpr int WIN = WROWS * 128;                  // one window buffer (64 channels)
+    static constexpr int WT = BN * 128;                      // 16 KiB per W tile
+    static constexpr int LDS = 2 * WIN + WSLOTS * WT;        // 128 / 80 KiB
+    static constexpr int PWIN = WROWS / 8 / NW;              // window pieces per wave (5 / 6)
+    static constexpr int PW = BN / 8 / NW;                   // W pieces per wave (2 / 4)
+    static_assert(PWIN * 8 * NW == WROWS && PW * 8 * NW == BN, "pieces split evenly over the waves");
+};
+#ifndef CONV7_BM
+#define CONV7_BM 128
+#endif
+__device__ __forceinline__ int sw7(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <int BM_, bool FUSED, bool RAW>
+__global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(ConvArgs a, ResUnitArgs u) {
+    using C7 = Conv7<BM_>;
+    constexpr int BM = C7::BM, BN = C7::BN;
+    __shared__ __attribute__((aligned(16))) char lds[C7::LDS];
+    char *win = lds, *wring = lds + 2 * C7::WIN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tilesN = a.N / BN;
+    const int64_t tilesM = (a.M + BM - 1) / BM;
+    const int64_t wg = xcd_remap(blockIdx.x, (int)(tilesM * tilesN));
+    const int64_t m0 = (wg / tilesN) * BM;
+    const int n0 = (int)(wg % tilesN) * BN;
+    const int dil = a.dil, Cin = a.Cin, K = 7 * Cin;
+    const int nch = Cin / 64, nk = 7 * nch;
+
+    auto stage_win = [&](int buf, int cc) {
+#pragma unroll
+        for (int i = 0; i < C7::PWIN; ++i) {
+            const int q = wave + C7::NW * i, row = q * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (row & 7);
+            const int64_t pos = m0 - 3 * dil + row;
+            const bf16_t *src = (row < BM + 6 * dil && pos >= 0 && pos < a.L_in)
+                                    ? a.in + pos * Cin + cc * 64 + c * 8 : a.zero + c * 8;
+            glds16(src, win + buf * C7::WIN + q * 1024);
+        }
+    };
+    auto stage_w = [&](int slot, int kt) {
+        const int cc = kt / 7, tap = kt - cc * 7;
+#pragma unroll
+        for (int i = 0; i < C7::PW; ++i) {
+            const int q = wave + C7::NW * i, row = q * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (row & 7);
+            glds16(a.W + (int64_t)(n0 + row) * K + tap * Cin + cc * 64 + c * 8, wring + slot * C7::WT + q * 1024);
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fc = lane >> 4;
+    const bool odd = fc & 1;
+    // residual-unit tail operands (x, b2) loaded up front: they land during the main
+    // loop (older than every DMA, so the loop's counted waits are unaffected)
+    uint4 xv[4][2], b2v[2];
+    if constexpr (FUSED) {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            const int n = wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
+            b2v[jp] = *(const uint4 *)(u.b2 + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t m = min(m0 + wm * 64 + i * 16 + fr, a.M - 1);
+                xv[i][jp] = *(const uint4 *)(u.x + m * 128 + n);
+            }
+        }
+    }
+    stage_win(0, 0);
+    stage_w(0, 0);
+    if (C7::WSLOTS == 3 && nk > 1) stage_w(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cc = kt / 7, tap = kt - cc * 7;
+        // own DMAs newer than W(kt): W(kt+1) (issued at kt−1) and a window refill issued at
+        // kt−1 or kt−2 (at a tap 0, right after that iteration's W refill)
+        // (3 W slots: W(kt+1) is newer, issued at kt−1; 2 slots: W(kt+1) is staged after
+        // this wait, and only a window refill at kt−1 is newer)
+        const bool w1 = C7::WSLOTS == 3 && kt + 1 < nk;
+        const bool wn1 = (kt >= 1 && (kt - 1) % 7 == 0 && (kt - 1) / 7 + 1 < nch) ||
+                         (C7::WSLOTS == 3 && kt >= 2 && (kt - 2) % 7 == 0 && (kt - 2) / 7 + 1 < nch);
+        if (w1 && wn1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C7::PW + C7::PWIN) : "memory");
+        else if (w1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C7::PW) : "memory");
+        else if (wn1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C7::PWIN) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + C7::WSLOTS - 1 < nk) stage_w((kt + C7::WSLOTS - 1) % C7::WSLOTS, kt + C7::WSLOTS - 1);
+        if (tap == 0 && cc + 1 < nch) stage_win((cc + 1) & 1, cc + 1);
+        const char *wb = win + (cc & 1) * C7::WIN, *tb = wring + (kt % C7::WSLOTS) * C7::WT;
+        const int rb = wm * 64 + tap * dil + fr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 xf[4], wf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xf[i] = *(const bf16x8 *)(wb + sw7(rb + i * 16, ks * 4 + fc));
+                wf[i] = *(const bf16x8 *)(tb + sw7(wn * 64 + i * 16 + fr, ks * 4 + fc));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    if constexpr (!FUSED) {
+        // conv output → bf16 (+bias) → Snake → out_s (the next conv's input)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = m0 + wm * 64 + i * 16 + fr;
+            if (m >= a.M) continue;
+#pragma unroll
+            for (int jp = 0; jp < 2; ++jp) {
+                float o[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                const int n = n0 + wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
+                if (a.bias) {
+                    float bb[8];
+                    unpack8(*(const uint4 *)(a.bias + n), bb);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                }
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = rbf(o[r]);
+                float sn[8];
+                snake8(o, a.sa + n, a.sib + n, sn);
+                *(uint4 *)(a.out_s + m * a.N + n) = pack8(sn);
+            }
+        }
+    } else {
+        // residual unit tail (C = 128): every wave done with the window / ring
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        constexpr int YH = BM * 128;    // y_s image: 2 k-halves × [BM rows][128 B]
+        char *ys = lds;
+        char *w2 = lds + 2 * YH;        // W2: 2 k-halves × [128 rows][128 B] = 32 KiB
+        static_assert(2 * YH + 32768 <= C7::LDS, "residual-unit tail must fit the LDS");
+        // W2 [128][128] → 2 k-halves: 32 glds
+#pragma unroll
+        for (int i = 0; i < 32 / C7::NW; ++i) {
+            const int qq = wave + C7::NW * i;  // 0..31: half = qq >> 4, rows 8(qq&15)..+7
+            const int h = qq >> 4, r = (qq & 15) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (r & 7);
+            glds16(u.W2 + (int64_t)r * 128 + h * 64 + c * 8, w2 + h * 16384 + (qq & 15) * 1024);
+        }
+        // epilogue 1: y_s = snake2(bf16(acc + b1)) → LDS (A image of the k=1 GEMM)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = wm * 64 + i * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = wn * 64 + j * 16 + fc * 4;
+                float bb[4];
+                unpack4(*(const uint2 *)(a.bias + n), bb);
+                const float4 sa = *(const float4 *)(a.sa + n);
+                const float4 sb = *(const float4 *)(a.sib + n);
+                const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
+                float o[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + bb[r]), sav[r], sbv[r]);
+                const int h = n >> 6, cc = (n & 63) >> 3;
+                *(uint2 *)(ys + h * YH + sw7(row, cc) + (n & 7) * 2) = pack4(o);
+                acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // k=1 GEMM: K = 128 = 2 halves × 2 k-steps
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 xf[4], wf[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    xf[i] = *(const bf16x8 *)(ys + h * YH + sw7(wm * 64 + i * 16 + fr, ks * 4 + fc));
+                    wf[i] = *(const bf16x8 *)(w2 + h * 16384 + sw7(wn * 64 + i * 16 + fr, ks * 4 + fc));
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+            }
+        // epilogue 2: x' = x + bf16(acc + b2); raw (optional) + snake_next
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = m0 + wm * 64 + i * 16 + fr;
+            if (m >= a.M) continue;
+#pragma unroll
+            for (int jp = 0; jp < 2; ++jp) {
+                float o[8], bb[8], rr[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                const int n = wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
+                unpack8(b2v[jp], bb);
+                unpack8(xv[i][jp], rr);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+                if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
+                float sn[8];
+                snake8(o, u.sa_next + n, u.sib_next + n, sn);
+                *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+            }
+        }
+    }
+}
+
 // Final decoder conv (Cout = 2 audio channels, k=7, pad 3, no bias) on the
 // already-snaked input; fp32 channels-first output [2][L].  One block = 256
 // output positions; the 262-row halo window is staged channel-major in LDS so
@@ -476,6 +716,17 @@ __global__ void cast_bf16_f32_kernel(const bf16_t *s, float *d, int64_t n) {
     if (i < n) d[i] = bf2f(s[i]);
 }
 
+// ACEHIP_CONV7=0 keeps the k=7 convolutions on the im2col conv_gemm / resunit128
+// kernels (A/B knob for the halo-staged conv7_kernel)
+bool use_conv7() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_CONV7");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 }  // namespace
 
 int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
@@ -486,6 +737,14 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
     if (!a.out && !a.out_s) return fail(-1, "conv_gemm: no output");
     if (!a.zero) return fail(-1, "conv_gemm: zero page");
     if (a.out_s && (!a.sa || !a.sib)) return fail(-1, "conv_gemm: snake params");
+    if (use_conv7() && phases == 1 && a.taps == 7 && a.a_stride == 1 && a.c_stride == 1 && a.c_off == 0 &&
+        a.a_off == -3 * a.dil && a.dil <= 9 && a.L_out == a.M && a.L_in == a.M && !a.res && !a.out && a.out_s) {
+        const int64_t t7 = ((a.M + CONV7_BM - 1) / CONV7_BM) * (a.N / 128);
+        if (t7 >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
+        conv7_kernel<CONV7_BM, false, false><<<(unsigned)t7, CONV7_BM * 2, 0, s>>>(a, ResUnitArgs{});
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
     if (tiles >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
     dim3 grid((unsigned)tiles, phases);
@@ -505,6 +764,13 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
     const ConvArgs &a = u.c1;
     if (a.Cin != 128 || a.N != 128 || a.taps != 7 || !a.zero || !a.bias || !a.sa) return fail(-1, "resunit128: args");
     if (u.x == u.out_s || a.in == u.out_s) return fail(-1, "resunit128: out_s must not alias x / x_s");
+    if (use_conv7() && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
+        const int64_t t7 = (a.M + CONV7_BM - 1) / CONV7_BM;
+        if (u.keep_raw) conv7_kernel<CONV7_BM, true, true><<<(unsigned)t7, CONV7_BM * 2, 0, s>>>(a, u);
+        else conv7_kernel<CONV7_BM, true, false><<<(unsigned)t7, CONV7_BM * 2, 0, s>>>(a, u);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     const int64_t tiles = (a.M + 127) / 128;
     if (tiles >= (1ll << 31)) return fail(-1, "resunit128: grid too large");
     if (u.keep_raw) resunit128_kernel<true><<<(unsigned)tiles, 256, 0, s>>>(u);
