@@ -68,6 +68,7 @@ def parse():
     p.add_argument("--repaint-end", type=float, default=120.0)
     p.add_argument("--text-len", type=int, default=128)
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    p.add_argument("--pmc-derived-json", default=os.path.join(REPO, "profiles", "pmc_derived.json"))
     p.add_argument("--dry-run", action="store_true",
                    help="CPU ranks over gloo with a stand-in song: exercises the launcher / timing / "
                         "max-over-ranks / JSON path without a GPU")
@@ -404,6 +405,19 @@ def main():
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4) if gbs else None,
                     "algorithmic_bytes": sw_bytes}
     roofline.update({"avg_launch_us": round(sw_ms * 1e3, 1), "launches": n_sw, "traffic": traffic})
+    # MFMA-busy counter and effective clock of the roofline kernel's main launch, from the
+    # committed counter pass of this shape (tools/gpu_prof.sh → tools/pmc_derived.py):
+    # frac above prices against the 2.4 GHz peak, frac_at_clock against the clock the chip held
+    try:
+        with open(args.pmc_derived_json) as f:
+            der = json.load(f).get("gemm_pp_kernel<256, 3> grid=516096") if M == 6000 else None
+        if der and sw_tflops:
+            clk = der.get("clock_GHz")
+            roofline.update({"mfma_busy_frac_pmc": der["mfma_busy_frac"], "clock_GHz_pmc": clk,
+                             "frac_at_clock": round(sw_tflops / (PEAK_BF16_TFLOPS * clk / 2.4), 4) if clk else None,
+                             "pmc_source": "profiles/pmc_derived.json"})
+    except Exception:
+        pass
     kernels = {k: {"launches": n, "avg_us": (ms / n * 1e3 if n else None)} for k, (n, ms) in prof_all.items()}
 
     out = {

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Derived per-kernel MFMA figures from a SQ/GRBM counter pass and the kernel-trace
+stats of the same code (MI355X_MICROARCH.md 'DVFS give-back' and §rocprofv3):
+  mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+  clock_GHz      = (GRBM_GUI_ACTIVE / 8) / average kernel duration (trace stats)
+  peak_at_clock  = 2.5 PF x clock / 2.4 GHz (bf16 dense)
+usage: pmc_derived.py PMC_SQ_JSON KERNEL_STATS_MD OUT_JSON"""
+import json
+import re
+import sys
+
+pmc = json.load(open(sys.argv[1]))
+avg = {}
+for line in open(sys.argv[2]):
+    m = re.match(r"\| `(.+?)` \| (\d+) \| [\d.]+ \| ([\d.]+) \|", line)
+    if m:
+        name = m.group(1).replace("x1x1", "").replace("x2x1", "")
+        avg[name] = float(m.group(3))
+out = {}
+for k, v in pmc.items():
+    g = v.get("GRBM_GUI_ACTIVE", 0)
+    if not g or not v.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+        continue
+    row = {"mfma_busy_frac": round(v["SQ_VALU_MFMA_BUSY_CYCLES"] * 8 / (1024 * g), 4), "launches": v["launches"]}
+    us = avg.get(k)
+    if us:
+        clk = g / 8 / (us * 1e-6) / 1e9
+        row.update({"avg_us_trace": us, "clock_GHz": round(clk, 3), "peak_bf16_TFs_at_clock": round(2500 * clk / 2.4, 1)})
+    out[k] = row
+json.dump(out, open(sys.argv[3], "w"), indent=1)
+for k, r in sorted(out.items(), key=lambda kv: -kv[1]["mfma_busy_frac"])[:20]:
+    print(k[:70], r)
