@@ -634,13 +634,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 //            ∥ ds_reads of tile kt+1's k-step 0 → F0
 // so the MFMA pipe never waits for a fragment read, the DMA of a tile has one whole
 // K-tile (≈96 MFMAs) of lead, and two LDS buffers suffice.
-template <int BM, int EPI>
+template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
-    constexpr int BN = 256, TM = BM / 2, TN = 128, SM = TM / 16, SN = TN / 16;
+    constexpr int TM = BM / 2, TN = BN / 2, SM = TM / 16, SN = TN / 16;
     constexpr int ROWS = BM + BN, STAGE = ROWS * 128;
+    // ring depth: 3 tile buffers when they fit (a refill's DMA then has two K-tiles of lead,
+    // enough for HBM-cold weights), else 2 (one K-tile of lead)
+    constexpr int NS = 3 * STAGE <= 160 * 1024 ? 3 : 2;
     constexpr int PW = ROWS / 32;                              // glds per wave per K-tile
     static_assert(ROWS % 32 == 0, "staging must split evenly over 4 waves");
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -696,10 +699,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
             }
     };
     auto none = [](int) {};
-    // the wait is the builtin (vmcnt(0) expcnt(7) lgkmcnt(0)), so the compiler's own
-    // waitcnt pass knows every read before it has retired and adds none after it
+    // the wait is the builtin (vmcnt((NS−2)·PW) expcnt(7) lgkmcnt(0): tile kt+1 landed,
+    // the NS−2 newer refills still in flight), so the compiler's own waitcnt pass knows
+    // every read before it has retired and adds none after it
+    constexpr int VM = (NS - 2) * PW;
+    static_assert(VM < 64, "vmcnt field");
+    constexpr int WAIT_ENC = 0x0070 | (VM & 15) | ((VM >> 4) << 14);
     auto bar = [] {
-        __builtin_amdgcn_s_waitcnt(0x0070);
+        __builtin_amdgcn_s_waitcnt(WAIT_ENC);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
@@ -714,15 +721,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     // accumulators between copies with VALU instructions that the asm MFMAs — opaque
     // to the hazard recognizer — would read without the required wait states.
     const int nk = a.K / BK;
+    // prologue: tiles 0..NS−1 (clamped: duplicates past the last tile keep the count
+    // uniform), tile 0 landed
 #pragma unroll
-    for (int i = 0; i < PW; ++i) stage1(0, 0, i);
-    if (nk > 1) {
+    for (int t = 0; t < NS; ++t)
 #pragma unroll
-        for (int i = 0; i < PW; ++i) stage1(1, BK, i);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+        for (int i = 0; i < PW; ++i) stage1(t, min(t, nk - 1) * BK, i);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd(lds, 0, x0, w0);
@@ -730,19 +735,21 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     constexpr int EVERY = W4_DMA_EVERY > 0 ? W4_DMA_EVERY : SM * SN / PW, FIRST = W4_DMA_FIRST;
     static_assert(FIRST + EVERY * (PW - 1) < SM * SN, "refill pieces must fit in half B");
     for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt % NS, nxt = (kt + 1) % NS;
         __builtin_amdgcn_s_waitcnt(0xC07F);
-        rd(lds + (kt & 1) * STAGE, 1, x1, w1);
+        rd(lds + cur * STAGE, 1, x1, w1);
         mm(x0, w0, none);
         bar();
-        const int kr = min(kt + 2, nk - 1) * BK;
+        // refill of this tile's buffer (every wave is past its reads) with tile kt+NS
+        const int kr = min(kt + NS, nk - 1) * BK;
         if constexpr (FIRST < 0) {
 #pragma unroll
-            for (int i = 0; i < PW; ++i) stage1(kt & 1, kr, i);
+            for (int i = 0; i < PW; ++i) stage1(cur, kr, i);
         }
-        rd(lds + ((kt + 1) & 1) * STAGE, 0, x0, w0);
+        rd(lds + nxt * STAGE, 0, x0, w0);
         mm(x1, w1, [&](int n) {
             if (FIRST >= 0 && n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW)
-                stage1(kt & 1, kr, (n - FIRST) / EVERY);
+                stage1(cur, kr, (n - FIRST) / EVERY);
         });
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -750,6 +757,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     // before their accumulators are read
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     if constexpr (EPI == EPI_HEADPOST) {
+        static_assert(BN == 256, "head-post tiles hold two 128-column heads");
         headpost_epilogue<BM, 4, sizeof(lds)>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
             for (int i = 0; i < SM; ++i)
@@ -764,18 +772,18 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     }
 }
 
-template <int BM>
+template <int BM, int BN = 256>
 int launch_w4(const GemmArgs &a, hipStream_t s) {
-    if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
-    const int tiles = ((a.M + BM - 1) / BM) * (a.N / 256);
+    if (a.N % BN) return fail(-1, "gemm: N not a multiple of the 4-wave tile");
+    const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
     switch (a.epi) {
-        case EPI_STORE: gemm_w4_kernel<BM, EPI_STORE><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_GATED_RES: gemm_w4_kernel<BM, EPI_GATED_RES><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_RES: gemm_w4_kernel<BM, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_SWIGLU: gemm_w4_kernel<BM, EPI_SWIGLU><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_STORE: gemm_w4_kernel<BM, BN, EPI_STORE><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_w4_kernel<BM, BN, EPI_GATED_RES><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_RES: gemm_w4_kernel<BM, BN, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_SWIGLU: gemm_w4_kernel<BM, BN, EPI_SWIGLU><<<tiles, 256, 0, s>>>(a); break;
         case EPI_HEADPOST:
-            if constexpr (BM == 192) {
-                gemm_w4_kernel<BM, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
+            if constexpr (BM == 192 && BN == 256) {
+                gemm_w4_kernel<BM, BN, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
                 break;
             }
             return fail(-1, "gemm: the head-post epilogue needs the 192-row tile");
@@ -795,11 +803,11 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_SWIGLU: gemm_pp_kernel<BM, EPI_SWIGLU><<<tiles, 512, 0, s>>>(a); break;
         case EPI_HEADPOST:
-            if constexpr (BM == 192) {
+            if constexpr (BM == 192 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
                 break;
             }
-            return fail(-1, "gemm: head-post epilogue needs the 192-row ping-pong tile");
+            return fail(-1, "gemm: head-post epilogue needs the 192- or 128-row ping-pong tile");
         default: return fail(-1, "gemm: bad epilogue");
     }
     HIP_TRY(hipGetLastError());
@@ -838,6 +846,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 9: return launch<192, 256, 2, 2, 2>(a, s);   // 4 waves (1/SIMD), 96x128 wave tile, acc in AGPRs
         case 10: return launch<256, 256, 2, 2, 2>(a, s);  // 4 waves (1/SIMD), 128x128 wave tile
         case 11: return launch_w4<192>(a, s);             // 4 waves, 96x128 wave tile, pipelined fragments
+        case 12: return launch_pp<128>(a, s);             // ping-pong 128x256 (96 KiB), 64x64 wave tiles
+        case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
         default: return fail(-1, "gemm: bad variant");
     }
 }
@@ -875,7 +885,24 @@ static bool use_w4() {
     return v == 1;
 }
 
+// Half-chip grids (M ≈ 3000: the conditional rows' cross-Q / cross-O): the four-wave
+// 192×128 tile with a 3-deep ring fills the chip in one round (16 × 16 tiles at
+// N = 2048) where the 128² tile runs 0.75 of a 2-blocks-per-CU round: 34–35 → 31 µs,
+// hot or cold weights (tools/bench_gemm.py, r02).  ACEHIP_GEMM_W4S=0 disables it.
+static bool use_w4s(int64_t M, int N) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_GEMM_W4S");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (v != 1 || N % 128) return false;
+    const int cus = num_cus();
+    const int64_t t = ((M + 191) / 192) * (N / 128);
+    return t <= cus && t * 4 >= (int64_t)cus * 3;
+}
+
 int gemm_pick_variant(int64_t M, int N) {
+    if (use_w4s(M, N) && (N % 256 || ((M + 191) / 192) * (N / 256) <= num_cus() / 2)) return 13;
     if (N % 256) return 0;
     const int cus = num_cus();
     const int64_t t7 = ((M + 255) / 256) * (N / 256), t8 = ((M + 191) / 192) * (N / 256);
@@ -997,7 +1024,7 @@ int gemm(const GemmArgs &a, hipStream_t s) {
             st.bias = nullptr;
             st.C = (bf16_t *)a.ws;
             st.ldc = a.N;
-            int rc = gemm_variant(st, 0, s);
+            int rc = gemm_variant(st, use_w4s(a.M, a.N) ? 13 : 0, s);
             if (rc) return rc;
             HeadPostArgs hh = a.hp;
             hh.src = st.C;
@@ -1014,7 +1041,7 @@ int gemm(const GemmArgs &a, hipStream_t s) {
             if (rc <= 0) return rc;   // split done (0) or failed (< 0); 1 = not applicable
         }
     }
-    if ((v == 3 || v >= 5) && a.N % 256) v = 0;   // (11, 12 too)
+    if ((v == 3 || (v >= 5 && v != 13)) && a.N % 256) v = 0;   // (13 needs N % 128 only)
     return gemm_variant(a, v, s);
 }
 
