@@ -34,6 +34,7 @@
 // Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P).  Online softmax in the exp2 domain;
 // masked scores use a finite power-of-two sentinel (a row whose first tiles are
 // fully masked accumulates garbage that the first real tile's rescale zeroes).
+#include <type_traits>
 #include "kernels.h"
 
 namespace acehip {
@@ -47,12 +48,6 @@ namespace {
 #endif
 #ifndef ATT_TAU
 #define ATT_TAU 8.0f       // lazy-rescale threshold (0: rescale on every new max)
-#endif
-#ifndef ATT_RING_BAND
-#define ATT_RING_BAND 2    // K/V ring depth (tiles) of band layers: D−1 tiles in flight behind a
-#endif                     // counted vmcnt (r02 A/B at 240 s: depth 2 53.7 µs, 3 56.3, 4 56.2)
-#ifndef ATT_RING_FULL
-#define ATT_RING_FULL 2    // full / cross / causal / key-masked: one tile ahead (L2-warm K/V)
 #endif
 
 constexpr int QB = 128;    // queries per workgroup
@@ -88,22 +83,27 @@ __device__ __forceinline__ bf16x8 ds_read_b128(const char *lds_ptr) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
     return r;
 }
-// LDS reads at (per-lane offset + wave-uniform offset): the uniform part (ring slot, row
-// block) lives in an SGPR and is added inside the asm, so the compiler cannot hoist one
-// VGPR address per (slot, fragment) out of the tile loop — that costs ~50 VGPRs it has
-// to spill.  The per-lane parts (swizzled chunk offsets) are 8 VGPRs for K, 8 for V.
-__device__ __forceinline__ bf16x8 ds_read_b128_at(uint32_t lane_off, uint32_t uni_off) {
+// LDS reads at (per-lane offset VGPR + compile-time immediate): the per-lane parts
+// (swizzled chunk offsets) are 8 VGPRs for K and 8 for V; the ring slot and the row
+// block are the instruction's 16-bit offset field (the tile loop is unrolled by the
+// two ring slots so both are constants) — no address VALU per read, and no hoisted
+// VGPR address per (slot, fragment), which had cost ~50 VGPRs and spills.
+template <int OFF>
+__device__ __forceinline__ bf16x8 ds_read_b128_imm(uint32_t lane_off) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
     bf16x8 r;
-    uint32_t a;
-    asm volatile("v_add_u32 %1, %2, %3\n\tds_read_b128 %0, %1" : "=v"(r), "=&v"(a) : "s"(uni_off), "v"(lane_off));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(lane_off), "n"(OFF));
     return r;
 }
-__device__ __forceinline__ s16x4 ds_read_tr16_at(uint32_t lane_off, uint32_t uni_off) {
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_read_tr16_imm(uint32_t lane_off) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
     s16x4 r;
-    uint32_t a;
-    asm volatile("v_add_u32 %1, %2, %3\n\tds_read_b64_tr_b16 %0, %1" : "=v"(r), "=&v"(a) : "s"(uni_off), "v"(lane_off));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lane_off), "n"(OFF));
     return r;
 }
+template <int V>
+using IC = std::integral_constant<int, V>;
 // s_waitcnt lgkmcnt(0) that the listed fragments depend on (nothing using them can be
 // scheduled above it)
 __device__ __forceinline__ void lgkm_wait8(bf16x8 (&f)[8]) {
@@ -118,7 +118,7 @@ __device__ __forceinline__ int kvoff(int row, int ch) {
 // NREP = query heads per KV head handled by one workgroup (GQA sharing:
 // each K/V tile is staged once for all NREP heads).  4 waves × 32 queries
 // per head → QB = 128 queries per head per workgroup.
-template <int NREP, int D>
+template <int NREP>
 __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *__restrict__ q,
                                                                   const bf16_t *__restrict__ k,
                                                                   const bf16_t *__restrict__ v,
@@ -128,9 +128,10 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const uint8_t *__restrict__ kmask) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
-    constexpr int NBUF = D;                        // K/V ring slots (tiles)
-    static_assert(D >= 2 && D <= 4, "ring depth");
-    constexpr int GPW = 32 / (NT / 64);            // LDS-DMA instructions per wave per tile
+    // K/V ring of 2 slots: tile j+1 is staged while tile j is computed (3- and 4-deep
+    // rings with counted vmcnt measured slower on every layer kind, r02: band 53.7 µs at
+    // depth 2 vs 56.3 / 56.2 at 3 / 4; full and cross likewise)
+    constexpr int NBUF = 2;
     __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
@@ -218,26 +219,28 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
     uint32_t koff[8], voff[4][2];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) koff[s] = kvoff(r, 2 * s + hh);
+    for (int s = 0; s < 8; ++s) koff[s] = lds_base + kvoff(r, 2 * s + hh);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int h8 = 0; h8 < 2; ++h8)
-            voff[dt][h8] = kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+            voff[dt][h8] = lds_base + kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
     // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads.  The reads are issued by
     // inline asm: hipcc's waitcnt pass treats its own ds_read_tr builtin as an LDS read
     // that may alias the in-flight LDS-DMA refills and waits vmcnt(0) before it (every
     // tile, draining the ring); the asm reads are waited explicitly (lgkmcnt(0) bound to
     // their results, so no MFMA can move above the wait)
-    auto pv_reads = [&](uint32_t vbase, int dt, s16x4 (&rd)[2][2][2]) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const uint32_t ub = vbase + (32 * t + 16 * s) * 256;
-                rd[t][s][0] = ds_read_tr16_at(voff[dt][0], ub);
-                rd[t][s][1] = ds_read_tr16_at(voff[dt][1], ub);
-            }
+    // VB: the V half of the ring slot (compile-time); key rows +32t +16s are immediates too
+    auto pv_reads = [&](auto VBC, int dt, s16x4 (&rd)[2][2][2]) {
+        constexpr int VB = decltype(VBC)::value;
+        rd[0][0][0] = ds_read_tr16_imm<VB>(voff[dt][0]);
+        rd[0][0][1] = ds_read_tr16_imm<VB>(voff[dt][1]);
+        rd[0][1][0] = ds_read_tr16_imm<VB + 16 * 256>(voff[dt][0]);
+        rd[0][1][1] = ds_read_tr16_imm<VB + 16 * 256>(voff[dt][1]);
+        rd[1][0][0] = ds_read_tr16_imm<VB + 32 * 256>(voff[dt][0]);
+        rd[1][0][1] = ds_read_tr16_imm<VB + 32 * 256>(voff[dt][1]);
+        rd[1][1][0] = ds_read_tr16_imm<VB + 48 * 256>(voff[dt][0]);
+        rd[1][1][1] = ds_read_tr16_imm<VB + 48 * 256>(voff[dt][1]);
     };
     auto pv_wait = [](s16x4 (&rd)[2][2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)"
@@ -257,51 +260,40 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
             }
     };
     // P·V: the reads of d-block dt+1 are in flight during the MFMAs of dt
-    // ldsV: the V half of a ring slot (uniform)
-    auto pv = [&](const char *ldsV, const bf16x8 (&pf)[2][2]) {
-        const uint32_t vb = lds_base + (uint32_t)(ldsV - lds);
+    auto pv = [&](auto VBC, const bf16x8 (&pf)[2][2]) {
         s16x4 ra[2][2][2], rb[2][2][2];
-        pv_reads(vb, 0, ra);
+        pv_reads(VBC, 0, ra);
         pv_wait(ra);
-        pv_reads(vb, 1, rb);
+        pv_reads(VBC, 1, rb);
         pv_mfma(0, ra, pf);
         pv_wait(rb);
-        pv_reads(vb, 2, ra);
+        pv_reads(VBC, 2, ra);
         pv_mfma(1, rb, pf);
         pv_wait(ra);
-        pv_reads(vb, 3, rb);
+        pv_reads(VBC, 3, rb);
         pv_mfma(2, ra, pf);
         pv_wait(rb);
         pv_mfma(3, rb, pf);
     };
 
-    // wait until tile `need` landed: own DMAs retired down to the `newer` tiles staged
-    // after it (vmcnt counts this wave's GPW LDS-DMAs per tile), own LDS reads retired;
-    // then the barrier publishes the tile to every wave and retires the current tile's
-    // reads (WAR for the refill of its slot) — a raw s_barrier: __syncthreads() would
-    // add a full vmcnt(0) drain
-    auto tile_barrier = [&](int newer) {
-        if (D >= 4 && newer >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GPW) : "memory");
-        else if (D >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // end-of-tile wait: own DMAs of the next tile landed, own LDS reads retired; then the
+    // barrier publishes the tile to every wave and retires the current tile's reads (WAR
+    // for the refill of its slot) — a raw s_barrier: __syncthreads() would add a full
+    // vmcnt(0) drain
+    auto tile_barrier = [&] {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
 
-    // ring of D slots: tiles 0..D−2 staged up front; iteration it stages tile it+D−1 into
-    // the slot of tile it−1 (its last reads retired before the barrier that ended
-    // iteration it−1) and ends waiting for tile it+1 with min(D−2, …) newer tiles in flight
-#pragma unroll
-    for (int t = 0; t < D - 1; ++t)
-        if (t < ntiles) stage_tile((t_first + t) * KT, t);
-    tile_barrier(min(D - 2, ntiles - 1));
-    for (int it = 0; it < ntiles; ++it) {
+    // one tile; SLOT (compile-time: the loop is unrolled by the two ring slots) is the
+    // ring slot holding tile it, so every LDS address offset is an immediate
+    auto tile = [&](int it, auto SLOTC) {
+        constexpr int SLOT = decltype(SLOTC)::value;
+        constexpr int KB = SLOT * 2 * TILE, VB = KB + TILE;
         const int kv0 = (t_first + it) * KT;
-        const int cur = it % NBUF;
-        if (it + D - 1 < ntiles) stage_tile(kv0 + (D - 1) * KT, (it + D - 1) % NBUF);
-        const char *ldsK = lds + cur * 2 * TILE;
-        const char *ldsV = ldsK + TILE;
+        if (it + 1 < ntiles) stage_tile(kv0 + KT, SLOT ^ 1);   // tile it−1's slot: read by nobody now
         // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
         // skipped (the wave still joins the barrier); one entirely inside needs no mask
         const bool outside = (window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window)) ||
@@ -310,8 +302,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                               (causal ? kv0 + KT - 1 <= q0
                                       : (window < 0 || (kv0 >= q0 + 31 - window && kv0 + KT - 1 <= q0 + window)));
         if (outside) {
-            tile_barrier(min(D - 2, ntiles - 2 - it));
-            continue;
+            tile_barrier();
+            return;
         }
 
         // Sᵀ tiles: keys 32t..32t+31 × this wave's 32 queries
@@ -319,13 +311,12 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         // during the MFMAs of t=0
         f32x16 st[2];
         {
-            const uint32_t kbase = lds_base + cur * 2 * TILE;
             bf16x8 k0[8], k1[8];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) k0[s] = ds_read_b128_at(koff[s], kbase);
+            for (int s = 0; s < 8; ++s) k0[s] = ds_read_b128_imm<KB>(koff[s]);
             lgkm_wait8(k0);
 #pragma unroll
-            for (int s = 0; s < 8; ++s) k1[s] = ds_read_b128_at(koff[s], kbase + 32 * 256);
+            for (int s = 0; s < 8; ++s) k1[s] = ds_read_b128_imm<KB + 32 * 256>(koff[s]);
 #pragma unroll
             for (int j = 0; j < 16; ++j) { st[0][j] = 0.f; st[1][j] = 0.f; }
 #pragma unroll
@@ -393,9 +384,17 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
             for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
-        pv(ldsV, pf);
-        tile_barrier(min(D - 2, ntiles - 2 - it));
+        pv(IC<VB>{}, pf);
+        tile_barrier();
+    };
+    if (ntiles > 0) stage_tile(t_first * KT, 0);
+    tile_barrier();
+    int it = 0;
+    for (; it + 1 < ntiles; it += 2) {
+        tile(it, IC<0>{});
+        tile(it + 1, IC<1>{});
     }
+    if (it < ntiles) tile(it, IC<0>{});
 
     if (nsplit > 1) {
         // publish this part's (O, m, l) in lane order, then take a ticket; the last
@@ -517,13 +516,10 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
     }
     const int grid = sp.full + (units - sp.full) * sp.nsplit;
-    const bool band = window >= 0 && !kmask;
-    if (nrep == 2 && band) {
-        attn_fwd_kernel<2, ATT_RING_BAND><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
-    } else if (nrep == 2) {
-        attn_fwd_kernel<2, ATT_RING_FULL><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
+    if (nrep == 2) {
+        attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else if (nrep == 1) {
-        attn_fwd_kernel<1, 2><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
+        attn_fwd_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else {
         return fail(-1, "attention: heads/kv_heads must be 1 or 2");
     }
