@@ -43,6 +43,9 @@ namespace {
 #ifndef ATT_XCD
 #define ATT_XCD 1          // XCD-aware block → work-unit remap
 #endif
+#ifndef ATT_DEFER
+#define ATT_DEFER 0        // SIMD partners out of phase: waves 4-7 run each tile's P·V one tile late
+#endif                     // (3-slot ring) — A/B switch: measured 171 → 191 µs (r02), off
 #ifndef ATT_PRIO
 #define ATT_PRIO 1         // static s_setprio 1 for the younger half (waves 4-7)
 #endif
@@ -128,11 +131,15 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
                                                                   const uint8_t *__restrict__ kmask) {
     constexpr int NT = 256 * NREP;
     constexpr int TILE = KT * 256;                 // one K or V tile: 64 rows × 256 B
-    // K/V ring of 2 slots: tile j+1 is staged while tile j is computed (3- and 4-deep
-    // rings with counted vmcnt measured slower on every layer kind, r02: band 53.7 µs at
-    // depth 2 vs 56.3 / 56.2 at 3 / 4; full and cross likewise)
-    constexpr int NBUF = 2;
-    __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];   // [buf][K|V]
+    // K/V ring: tile j+1 is staged while tile j is computed; 3 slots when the deferred half
+    // still reads V(j−1) during tile j (deeper rings with more tiles in flight measured
+    // slower on every layer kind, r02: band 53.7 µs at depth 2 vs 56.3 / 56.2 at 3 / 4)
+    constexpr bool DEFER = ATT_DEFER && NREP == 2;
+    constexpr int NBUF = DEFER ? 3 : 2;
+    // [K slot 0 .. NBUF−1 | V slot 0 .. NBUF−1]: the K and the V fragment reads each
+    // address their region from their own lane-offset base, so every slot offset fits
+    // the 16-bit ds offset field (3 slots of K|V interleaved would reach 96 KiB)
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, hh = lane >> 5;
     // work unit u = (b, kvh, q-block), q-block fastest; blocks past sp.full are the
@@ -194,14 +201,14 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     // logical chunk that kvoff() places there (the XOR is an involution).  Rows
     // past Sk are clamped to a real row: those keys are masked (K) or meet P = 0 (V).
     auto stage_tile = [&](int kv0, int buf) {
-        char *base = lds + buf * 2 * TILE;
 #pragma unroll
         for (int i = 0; i < 32 / (NT / 64); ++i) {
             const int c = wave * (32 / (NT / 64)) + i;
             const int isv = c >> 4, row = (c & 15) * 4 + (lane >> 4), pc = lane & 15;
             const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
             const int key = min(kv0 + row, Sk - 1);
-            glds16((isv ? vp : kp) + (int64_t)key * 128 + ch * 8, base + isv * TILE + (c & 15) * 1024);
+            glds16((isv ? vp : kp) + (int64_t)key * 128 + ch * 8,
+                   lds + (isv * NBUF + buf) * TILE + (c & 15) * 1024);
         }
     };
 
@@ -224,7 +231,8 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int h8 = 0; h8 < 2; ++h8)
-            voff[dt][h8] = lds_base + kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+            voff[dt][h8] = lds_base + NBUF * TILE +
+                           kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
     // Oᵀ[d][q] += Vᵀ·Pᵀ; Vᵀ fragments by transposed LDS reads.  The reads are issued by
     // inline asm: hipcc's waitcnt pass treats its own ds_read_tr builtin as an LDS read
     // that may alias the in-flight LDS-DMA refills and waits vmcnt(0) before it (every
@@ -287,13 +295,34 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
     };
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
 
-    // one tile; SLOT (compile-time: the loop is unrolled by the two ring slots) is the
-    // ring slot holding tile it, so every LDS address offset is an immediate
+    // SIMD partners (wave w and w+4 share a SIMD) are put out of phase: the younger half
+    // defers each tile's P·V into the next tile's interval, so within one barrier interval
+    // wave w runs [QKᵀ(j) | softmax(j) | P·V(j)] while wave w+4 runs [P·V(j−1) | QKᵀ(j) |
+    // softmax(j)]: two of the three segments pair MFMAs with the partner's softmax VALU
+    // instead of both waves issuing the same kind (MI355X_MICROARCH "Two waves per SIMD").
+    // P·V(j−1) precedes softmax(j)'s O rescale, so O is at tile j−1's max when it lands.
+    const bool defer = DEFER && __builtin_amdgcn_readfirstlane(wave) >= 4;
+    bool pending = false;          // deferred half: P of the last computed tile awaits P·V
+    int pend_slot = 0;
+    auto pv_slot = [&](int slot, const bf16x8 (&pfv)[2][2]) {
+        if (slot == 0) pv(IC<0>{}, pfv);
+        else if (slot == 1) pv(IC<TILE>{}, pfv);
+        else pv(IC<2 * TILE>{}, pfv);
+    };
+    // one tile; SLOT (compile-time: the loop is unrolled by the ring slots) is the ring
+    // slot holding tile it, so every LDS address offset is an immediate
     auto tile = [&](int it, auto SLOTC) {
         constexpr int SLOT = decltype(SLOTC)::value;
-        constexpr int KB = SLOT * 2 * TILE, VB = KB + TILE;
+        constexpr int KB = SLOT * TILE, VB = SLOT * TILE;    // K from koff, V from voff (region-biased)
+        constexpr int PREV = (SLOT + NBUF - 1) % NBUF;
         const int kv0 = (t_first + it) * KT;
-        if (it + 1 < ntiles) stage_tile(kv0 + KT, SLOT ^ 1);   // tile it−1's slot: read by nobody now
+        // refill: tile it+1 into the slot of tile it+1−NBUF, read by nobody now (with 3
+        // slots that is tile it−2, whose deferred P·V ran in iteration it−1)
+        if (it + 1 < ntiles) stage_tile(kv0 + KT, (SLOT + 1) % NBUF);
+        if (DEFER && pending) {                     // wave-uniform: the deferred half only
+            pv(IC<PREV * TILE>{}, pf);
+            pending = false;
+        }
         // band layers: a tile entirely outside this wave's |i−j| ≤ window band is
         // skipped (the wave still joins the barrier); one entirely inside needs no mask
         const bool outside = (window >= 0 && !km && (kv0 > q0 + 31 + window || kv0 + KT - 1 < q0 - window)) ||
@@ -384,17 +413,33 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
             for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) pf[t][s][j] = (__bf16)st[t][8 * s + j];
-        pv(IC<VB>{}, pf);
+        if (DEFER && defer) {
+            pending = true;
+            pend_slot = SLOT;
+        } else {
+            pv(IC<VB>{}, pf);
+        }
         tile_barrier();
     };
     if (ntiles > 0) stage_tile(t_first * KT, 0);
     tile_barrier();
     int it = 0;
-    for (; it + 1 < ntiles; it += 2) {
-        tile(it, IC<0>{});
-        tile(it + 1, IC<1>{});
+    if constexpr (NBUF == 3) {
+        for (; it + 2 < ntiles; it += 3) {
+            tile(it, IC<0>{});
+            tile(it + 1, IC<1>{});
+            tile(it + 2, IC<2>{});
+        }
+        if (it < ntiles) tile(it, IC<0>{});
+        if (it + 1 < ntiles) tile(it + 1, IC<1>{});
+    } else {
+        for (; it + 1 < ntiles; it += 2) {
+            tile(it, IC<0>{});
+            tile(it + 1, IC<1>{});
+        }
+        if (it < ntiles) tile(it, IC<0>{});
     }
-    if (it < ntiles) tile(it, IC<0>{});
+    if (DEFER && pending) pv_slot(pend_slot, pf);
 
     if (nsplit > 1) {
         // publish this part's (O, m, l) in lane order, then take a ticket; the last
