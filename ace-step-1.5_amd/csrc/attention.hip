@@ -47,7 +47,7 @@ namespace {
 #define ATT_DEFER 0        // SIMD partners out of phase: waves 4-7 run each tile's P·V one tile late
 #endif                     // (3-slot ring) — A/B switch: measured 171 → 191 µs (r02), off
 #ifndef ATT_PRIO
-#define ATT_PRIO 1         // static s_setprio 1 for the younger half (waves 4-7)
+#define ATT_PRIO 0         // static s_setprio 1 for the younger half (waves 4-7): r02 A/B 1-3 % slower, off
 #endif
 #ifndef ATT_TAU
 #define ATT_TAU 8.0f       // lazy-rescale threshold (0: rescale on every new max)
