@@ -46,6 +46,9 @@ namespace {
 #ifndef ATT_DEFER
 #define ATT_DEFER 0        // SIMD partners out of phase: waves 4-7 run each tile's P·V one tile late
 #endif                     // (3-slot ring) — A/B switch: measured 171 → 191 µs (r02), off
+#ifndef ATT_SPLIT_HEADS
+#define ATT_SPLIT_HEADS 1  // GQA pair split into two 4-wave workgroups for short KV loops
+#endif
 #ifndef ATT_PRIO
 #define ATT_PRIO 0         // static s_setprio 1 for the younger half (waves 4-7): r02 A/B 1-3 % slower, off
 #endif
@@ -122,7 +125,7 @@ __device__ __forceinline__ int kvoff(int row, int ch) {
 // each K/V tile is staged once for all NREP heads).  4 waves × 32 queries
 // per head → QB = 128 queries per head per workgroup.
 template <int NREP>
-__global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *__restrict__ q,
+__global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf16_t *__restrict__ q,
                                                                   const bf16_t *__restrict__ k,
                                                                   const bf16_t *__restrict__ v,
                                                                   bf16_t *__restrict__ o, int H, int KV,
@@ -155,8 +158,11 @@ __global__ __launch_bounds__(256 * NREP, 1) void attn_fwd_kernel(const bf16_t *_
         part = j % sp.nsplit;
         nsplit = sp.nsplit;
     }
-    const int qb = u % sp.nq, kvh = (u / sp.nq) % KV, b = u / (sp.nq * KV);
-    const int hq = kvh * NREP + (wave >> 2);
+    // head group hg of NREP query heads; hpw head groups share one KV head
+    const int hpw = H / (KV * NREP);
+    const int qb = u % sp.nq, hg = (u / sp.nq) % (KV * hpw), b = u / (sp.nq * KV * hpw);
+    const int kvh = hg / hpw;
+    const int hq = hg * NREP + (wave >> 2);
     const int qblk = qb * QB;
     const int q0 = qblk + (wave & 3) * 32;
     const int qi = q0 + r;
@@ -531,19 +537,28 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     if (B <= 0 || Sq <= 0) return 0;
     if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
     if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
-    const int nrep = H / KV;
+    const int grp = H / KV;
     const float sl2 = scale * 1.4426950408889634f;
     const int nq = (Sq + QB - 1) / QB;
-    const int units = nq * KV * B;
+    const int cus = num_cus_attn();
+    const int unit_tiles = (window >= 0 && !kmask) ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
+    // heads per workgroup: the GQA pair shares one 8-wave workgroup (K/V staged once per
+    // tile for both heads), or each head gets its own 4-wave workgroup, two per CU, whose
+    // SIMD partners run out of phase. Measured (r02, one box): band −3 %, cross −9 %,
+    // full (47 tiles: the doubled K/V staging dominates) +7 %, cross with fewer pair units
+    // than CUs (B = 1) +11 %, short split-KV cross slower.
+    const bool short_split = window < 0 && nq * KV * B * 2 <= cus && unit_tiles >= 4;
+    const bool split_heads = ATT_SPLIT_HEADS && grp == 2 && window != ATTN_CAUSAL &&
+                             unit_tiles < 24 && !short_split && nq * KV * B > cus;
+    const int nrep = split_heads ? 1 : grp;
+    const int units = nq * KV * (grp / nrep) * B;
     SplitArgs sp{nq, units, 1, nullptr, nullptr};
     // one workgroup per CU: a partial last round of whole units is replaced by
     // tail units split over ⌊CUs / tail⌋ KV ranges (1.5 rounds instead of 2 at
     // 384 units on 256 CUs)
-    const int cus = num_cus_attn();
     const int tail = units % cus;
     // only long KV loops pay for the partial write + merge (measured: full attention
     // at S = 3000, 47 tiles, −27 %; band (≈7 tiles) and cross (11 tiles) lose)
-    const int unit_tiles = (window >= 0 && !kmask) ? (QB + 2 * window) / KT + 1 : (Sk + KT - 1) / KT;
     if (window == ATTN_CAUSAL) {
         // causal (text encoder): whole units only — a KV-range part past the diagonal
         // would hold no valid key
@@ -552,7 +567,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.nsplit = min(4, cus / tail);
         sp.cnt = (int *)ws;
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
-    } else if (ws && nrep == 2 && window < 0 && units * 2 <= cus && unit_tiles >= 4) {
+    } else if (ws && nrep == 2 && short_split) {
         // short sequences (a few query blocks): every unit split over KV ranges so the
         // grid reaches the CUs (cross-attention of a 10 s song: 8 units → 40 parts)
         sp.full = 0;

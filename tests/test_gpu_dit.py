@@ -113,7 +113,8 @@ def _attn_ref(q, k, v, window):
 @pytest.mark.parametrize("B,H,KV,Sq,Sk,window", [(2, 4, 2, 300, 300, -1), (2, 4, 2, 300, 300, 8),
                                                   (1, 16, 8, 1000, 1000, 128), (2, 4, 2, 257, 641, -1),
                                                   (1, 2, 1, 50, 20, -1), (1, 2, 1, 3000, 3000, 128),
-                                                  # DiT shapes at 240 s: 384 units on 256 CUs → tail split
+                                                  # DiT shapes at 240 s: 384 units on 256 CUs → tail split (full),
+                                                  # GQA pair split into two 4-wave workgroups (band, cross)
                                                   (2, 16, 8, 3000, 3000, -1), (2, 16, 8, 3000, 3000, 128),
                                                   (2, 16, 8, 3000, 641, -1),
                                                   # 10 s song: 8 units → every unit KV-split
