@@ -22,15 +22,23 @@ struct ConvArgs {
 // fused residual unit at C = 128: c1 = the k=7 conv (in = x_s, sa/sib = snake2,
 // bias = b1); then x' = x + (W2·y_s + b2), written raw into x (keep_raw) and
 // snaked (sa_next/sib_next) into out_s
+// zero rows (of the widest stage, 2048 channels) kept in front of the VAE activation buffers:
+// the persistent residual-unit kernel reads the k=7 halo rows before the start from them
+constexpr int kActPadRows = 32;
 struct ResUnitArgs {
     ConvArgs c1;
     const bf16_t *W2, *b2;
+    const bf16_t *W2p;                           // W2 with columns permuted (permute_k1_weight) or null
+    int in_zero_pad;                             // c1.in is preceded by ≥ kActPadRows zero rows (ru7_kernel)
     bf16_t *x;
     bf16_t *out_s;
     const float *sa_next, *sib_next;
     int keep_raw;
 };
 int resunit128(const ResUnitArgs &u, hipStream_t s);
+// W2 [n_rows][128] → columns permuted within each 32-block so that the k=7 accumulator
+// layout is the k=1 MFMA's B operand (ru7_kernel): new 8g+e ← old e<4 ? 4g+e : 16+4g+e−4
+int permute_k1_weight(const bf16_t *w, bf16_t *wp, int n_rows, hipStream_t s);
 int conv_gemm(const ConvArgs &a, int phases, hipStream_t s);
 // final decoder conv: snaked NLC [L][Cin] → fp32 channels-first [Cout=2][L], k 7, no bias
 int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s);

@@ -23,6 +23,8 @@
 // the MFMAs of the current tile), XOR-swizzled for conflict-free ds_read_b128.
 #include "kernels.h"
 #include "conv.h"
+#include <algorithm>
+#include <type_traits>
 
 namespace acehip {
 namespace {
@@ -418,7 +420,8 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(Conv
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + C7::WSLOTS - 1 < nk) stage_w((kt + C7::WSLOTS - 1) % C7::WSLOTS, kt + C7::WSLOTS - 1);
+        if (kt + C7::WSLOTS - 1 < nk)
+            stage_w((kt + C7::WSLOTS - 1) % C7::WSLOTS, kt + C7::WSLOTS - 1);
         if (tap == 0 && cc + 1 < nch) stage_win((cc + 1) & 1, cc + 1);
         const char *wb = win + (cc & 1) * C7::WIN, *tb = wring + (kt % C7::WSLOTS) * C7::WT;
         const int rb = wm * 64 + tap * dil + fr;
@@ -540,6 +543,301 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(Conv
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent, software-pipelined Oobleck residual unit at C = 128 (vae_model.py:62-87):
+//   y_s = snake2(conv7_dil(x_s) + b1);  x' = x + (W2·y_s + b2);  out_s = snake_next(x')
+// conv7_kernel<FUSED> runs one tile per block; its per-tile tail (W2 staging, epilogue
+// parameter loads, the y_s LDS round trip, two barriers, the k=1 GEMM, the stores) measured
+// more than half of the kernel (r02: decode −11 ms with the tail skipped).  Here every block
+// walks a contiguous range of 128-row tiles:
+//  * each wave owns 32 rows × all 128 channels, so y_s never leaves registers: the k=7
+//    accumulators (lane: row fr, channels 16j + 4fc + r) ARE the B operand of the k=1 MFMA
+//    once W2's columns are permuted within each 32-block (permute_k1_kernel);
+//  * the W stream has 16 K-tiles per row tile — 14 k=7 (tap, 64-channel chunk) tiles, then
+//    W2's two 64-column halves — through a 2-slot ring that waves 0-2 refill one K-tile
+//    ahead (wrapping into the next tile's W(0)), so W2 arrives like any W tile;
+//  * wave 3 alone stages the input windows (x_s rows m0−3d … m0+127+3d: 182 rows × 64
+//    channels per chunk, chunk c in buffer c) a tile ahead: chunk 0 of tile t+1 behind
+//    K-tiles 7–12 (buffer 0 is free after K-tile 6), chunk 1 after the epilogue and behind
+//    K-tiles 0–3.  vmcnt is per wave: the W waves' one-K-tile waits never include a window
+//    piece, and wave 3 waits only where a chunk is consumed (K-tiles 0 and 7);
+//  * the epilogue parameters (b1, b2, both Snakes) sit in LDS; x (the residual) is loaded
+//    two K-tiles before its use.
+// LDS: 2 560 (parameters) + 2 × 23 296 (windows) + 2 × 16 KiB (W ring) = 80 KiB: two blocks
+// per CU, whose K-loops and epilogues interleave.
+namespace ru {
+constexpr int BM = 128, WROWS = 182, WINB = WROWS * 128, WT = 128 * 128, PAR = 2560;
+constexpr int LDS = 2 * WINB + 2 * WT + PAR;
+constexpr int NPW = (WROWS + 7) / 8;   // 23 window pieces (8 rows) per chunk; the last is 6 rows
+static_assert(LDS <= 81920, "two blocks per CU");
+}  // namespace ru
+
+// The kernel's LDS-DMA is inline asm (global_load_lds, saddr form: SGPR
+// base + one 32-bit VGPR lane offset) with explicit counted waits:
+//  * the builtin LDS-DMA forms either build a 64-bit VGPR address per piece (46 window + 16 W
+//    pieces per tile: hoisted and spilled, and every spill reload waits vmcnt(0)) or, for
+//    the buffer form, make the compiler wait vmcnt(0) before every LDS read;
+//  * the compiler, not seeing these loads, inserts no vmcnt waits for them (the x loads,
+//    which fill registers, stay compiler-visible).
+// M0 (the LDS destination) is set in the same asm; nothing else in this kernel uses M0.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ru_dma(const char *base, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(base)
+                 : "memory");
+}
+
+// window pieces [P0, P1) (8 rows each) of 64-channel chunk cc for the tile at m0, from input
+// row m0 − 3d + 8·P0 (≥ −27, and ≤ L_in + 181 at the end: the input carries zero rows in
+// front and zeroed / addressable rows behind, ResUnitArgs::in_zero_pad); lanes of rows
+// ≥ WROWS are masked off.  buf: LDS address; voff: (lane>>3)·256 + swizzled chunk + cc·128.
+template <int P0, int P1>
+__device__ __forceinline__ void ru_win(const ConvArgs &a, uint32_t buf, int64_t m0, uint32_t voff, int lane) {
+    const char *base = (const char *)(a.in + (m0 - 3 * a.dil + P0 * 8) * 128);
+#pragma unroll
+    for (int q = P0; q < P1; ++q) {
+        if (q * 8 + 8 <= ru::WROWS || (lane >> 3) < ru::WROWS - q * 8)
+            ru_dma(base, buf + q * 1024, voff + (q - P0) * 2048);
+    }
+}
+
+// W K-tile kt (0-13: W1 tap kt%7 of chunk kt/7; 14, 15: W2 column half kt−14) into the ring
+// slot at LDS address `slot`: 16 pieces of 8 rows, piece q by wave q % 3; voff1 / voff2: lane
+// offsets in the 1792-B W1 rows and the 256-B W2 rows
+__device__ __forceinline__ void ru_w(const ResUnitArgs &u, uint32_t slot, int kt, int wave, uint32_t voff1,
+                                     uint32_t voff2) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int q = wave + 3 * i;
+        if (q < 16) {
+            if (kt < 14) {
+                const int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
+                ru_dma((const char *)u.c1.W + q * 8 * 1792 + tap * 256 + cc * 128, slot + q * 1024, voff1);
+            } else {
+                ru_dma((const char *)u.W2p + q * 8 * 256 + (kt - 14) * 128, slot + q * 1024, voff2);
+            }
+        }
+    }
+}
+
+template <bool RAW>
+__global__ __launch_bounds__(256, 2) void ru7_kernel(ResUnitArgs u, int64_t ntiles) {
+    constexpr int RBM = ru::BM, WINB = ru::WINB, WT = ru::WT, NPW = ru::NPW;
+    __shared__ __attribute__((aligned(16))) char lds[ru::LDS];
+    const ConvArgs &a = u.c1;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool dma = wave == 3;
+    const int fr = lane & 15, fc = lane >> 4;
+    const bool odd = fc & 1;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
+    // parameters first: their per-lane reads then fold into the 16-bit ds offset field
+    // parameters first: their per-lane reads then fold into the 16-bit ds offset field
+    char *par = lds, *win = lds + ru::PAR, *wr = win + 2 * WINB;
+    const uint32_t win3 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds + ru::PAR;
+    const uint32_t wr3 = win3 + 2 * WINB;                                 // LDS-DMA destinations
+    float *psa2 = (float *)par, *psib2 = psa2 + 128, *psan = psa2 + 256, *psibn = psa2 + 384;
+    bf16_t *pb1 = (bf16_t *)(par + 2048), *pb2 = (bf16_t *)(par + 2304);
+    if (tid < 128) {
+        psa2[tid] = a.sa[tid]; psib2[tid] = a.sib[tid];
+        psan[tid] = u.sa_next[tid]; psibn[tid] = u.sib_next[tid];
+        pb1[tid] = a.bias[tid]; pb2[tid] = u.b2[tid];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);          // parameter loads retired before the first DMA
+    // DMA lane offsets: row lane>>3 of a piece, 16-B chunk swizzled by row & 7 (= lane>>3)
+    const int l3 = lane >> 3, lc = ((lane & 7) ^ l3) * 16;
+    const uint32_t vw0 = l3 * 256 + lc, vw1 = vw0 + 128;          // window chunk 0 / 1
+    const uint32_t vk1 = l3 * 1792 + lc, vk2 = l3 * 256 + lc;       // W1 / W2 rows
+    if (dma) {
+        ru_win<0, NPW>(a, win3, t0 * RBM, vw0, lane);
+        ru_win<0, 8>(a, win3 + WINB, t0 * RBM, vw1, lane);
+    } else {
+        ru_w(u, wr3, 0, wave, vk1, vk2);
+    }
+    // W fragment lane offsets: rows 16j + fr, 16-B chunk 4ks + fc (swizzled like the DMA)
+    const int wl[2] = {fr * 128 + ((fc ^ (fr & 7)) << 4), fr * 128 + (((4 + fc) ^ (fr & 7)) << 4)};
+
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t m0 = t * RBM;
+        const bool more = t + 1 < t1;
+        u32x4 xv[2][4];
+        bf16x8 yf[2][4];
+        auto ktile = [&](const int kt, auto SLOTC) {
+            constexpr int SLOT = decltype(SLOTC)::value;
+            // W waves: W(kt) (issued at kt−1) retired; younger only x (issued at 14 after W(15)).
+            // Wave 3: chunk 0 (K-tile 0; younger: chunk 1's first 8 pieces) or chunk 1 (K-tile 7).
+            if (!dma) {
+                if (kt == 15) __builtin_amdgcn_s_waitcnt(0x0078);       // vmcnt(8) lgkmcnt(0)
+                else __builtin_amdgcn_s_waitcnt(0x0070);
+            } else {
+                if (kt == 0) __builtin_amdgcn_s_waitcnt(0x0078);
+                else if (kt == 7) __builtin_amdgcn_s_waitcnt(0x0070);
+                else __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0) only
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (!dma) {
+                if (kt < 15 || more) ru_w(u, wr3 + (SLOT ^ 1) * WT, kt == 15 ? 0 : kt + 1, wave, vk1, vk2);
+            } else if (kt == 0) {
+                ru_win<8, 12>(a, win3 + WINB, m0, vw1, lane);
+            } else if (kt == 1) {
+                ru_win<12, 16>(a, win3 + WINB, m0, vw1, lane);
+            } else if (kt == 2) {
+                ru_win<16, 20>(a, win3 + WINB, m0, vw1, lane);
+            } else if (kt == 3) {
+                ru_win<20, NPW>(a, win3 + WINB, m0, vw1, lane);
+            } else if (more) {
+                if (kt == 7) ru_win<0, 4>(a, win3, m0 + RBM, vw0, lane);
+                else if (kt == 8) ru_win<4, 8>(a, win3, m0 + RBM, vw0, lane);
+                else if (kt == 9) ru_win<8, 12>(a, win3, m0 + RBM, vw0, lane);
+                else if (kt == 10) ru_win<12, 16>(a, win3, m0 + RBM, vw0, lane);
+                else if (kt == 11) ru_win<16, 20>(a, win3, m0 + RBM, vw0, lane);
+                else if (kt == 12) ru_win<20, NPW>(a, win3, m0 + RBM, vw0, lane);
+            }
+            if (kt == 14) {
+                // x (residual) rows of this wave: 8 loads, waited before epilogue 2
+                const char *xb = (const char *)(u.x + m0 * 128);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jp = 0; jp < 4; ++jp) {
+                        const int r = (int)min((int64_t)(32 * wave + 16 * i + fr), a.M - 1 - m0);
+                        const uint32_t off = (uint32_t)(r * 128 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8) * 2;
+                        xv[i][jp] = *(const u32x4 *)(xb + off);
+                    }
+            }
+            const char *tb = wr + SLOT * WT;
+            if (kt < 14) {
+                const int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
+                int dl = a.dil;
+                asm volatile("" : "+s"(dl));    // per-tap address math stays here (not hoisted out of the tile loop)
+                const int rb = 32 * wave + fr + tap * dl;
+                const char *wb = win + cc * WINB + rb * 128;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int xo = ((4 * ks + fc) ^ (rb & 7)) << 4;
+                    bf16x8 xf[2], wf[8];
+                    xf[0] = *(const bf16x8 *)(wb + xo);
+                    xf[1] = *(const bf16x8 *)(wb + 2048 + xo);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[ks]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+                }
+            } else {
+                constexpr int h = SLOT;       // K-tiles 14 / 15 sit in slots 0 / 1
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    bf16x8 wf[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[ks]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], yf[i][2 * h + ks], acc[i][j],
+                                                                                0, 0, 0);
+                }
+            }
+            if (kt == 13) {
+                // epilogue 1: y_s = snake2(bf16(acc + b1)) → the k=1 B fragments (k-step s =
+                // channel tiles 2s, 2s+1: lane group fc holds channels 32s + 4fc + {0-3, 16-19})
+                uint2 yv[2][8];
+                int pl = 4 * fc;
+                asm volatile("" : "+v"(pl));
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int n = 16 * j + pl;
+                    float b[4];
+                    unpack4(*(const uint2 *)(pb1 + n), b);
+                    const float4 sa = *(const float4 *)(psa2 + n), sb = *(const float4 *)(psib2 + n);
+                    const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        float o[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + b[r]), sav[r], sbv[r]);
+                        yv[i][j] = pack4(o);
+                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+                        yf[i][s] = __builtin_bit_cast(bf16x8, make_uint4(yv[i][2 * s].x, yv[i][2 * s].y,
+                                                                         yv[i][2 * s + 1].x, yv[i][2 * s + 1].y));
+            }
+        };
+        // K-tiles 0-11 in a loop; 12-15 peeled so that x and the y_s fragments are not
+        // loop-carried (they would pin 64 VGPRs through the whole K loop)
+#pragma unroll 1
+        for (int kt = 0; kt < 12; kt += 2) {
+            ktile(kt, std::integral_constant<int, 0>{});
+            ktile(kt + 1, std::integral_constant<int, 1>{});
+        }
+        ktile(12, std::integral_constant<int, 0>{});
+        ktile(13, std::integral_constant<int, 1>{});
+        ktile(14, std::integral_constant<int, 0>{});
+        ktile(15, std::integral_constant<int, 1>{});
+        // epilogue 2: x' = x + bf16(acc + b2) (raw, optional) and snake_next(x') → out_s.
+        // (x is a compiler-visible load: an asm load's destination registers may be copied by
+        // the register allocator before an asm wait retires them; the compiler's own wait
+        // here is vmcnt(0), which also retires the W waves' W(0) pieces of the next tile)
+        int64_t me = m0;
+        asm volatile("" : "+s"(me));
+        int pl2 = (odd ? 16 : 0) + (fc >> 1) * 8;
+        asm volatile("" : "+v"(pl2));
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+            const int n = 32 * jp + pl2;
+            float bb[8];
+            unpack8(*(const uint4 *)(pb2 + n), bb);
+            const float4 a0 = *(const float4 *)(psan + n), a1 = *(const float4 *)(psan + n + 4);
+            const float4 s0 = *(const float4 *)(psibn + n), s1 = *(const float4 *)(psibn + n + 4);
+            const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                float o[8], rr[8], sn[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                acc[i][2 * jp] = f32x4{0.f, 0.f, 0.f, 0.f};
+                acc[i][2 * jp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                unpack8(make_uint4(xv[i][jp].x, xv[i][jp].y, xv[i][jp].z, xv[i][jp].w), rr);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+                    sn[r] = snake1(o[r], av[r], sv[r]);
+                }
+                const int64_t m = me + 32 * wave + 16 * i + fr;
+                if (m < a.M) {
+                    if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
+                    *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+                }
+            }
+        }
+        // chunk 1 of the next tile: buffer 1 was last read at K-tile 13
+        if (dma && more) ru_win<0, 8>(a, win3 + WINB, m0 + RBM, vw1, lane);
+    }
+}
+
+__global__ void permute_k1_kernel(const bf16_t *w, bf16_t *wp, int n_rows) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n_rows * 128) return;
+    const int n = idx >> 7, k = idx & 127;
+    const int s = k >> 5, g = (k >> 3) & 3, e = k & 7;
+    wp[idx] = w[n * 128 + 32 * s + (e < 4 ? 4 * g + e : 16 + 4 * g + e - 4)];
 }
 
 // Final decoder conv (Cout = 2 audio channels, k=7, pad 3, no bias) on the
@@ -727,7 +1025,34 @@ bool use_conv7() {
     return v == 1;
 }
 
+// ACEHIP_RU7=0 keeps the C = 128 residual units on conv7_kernel<FUSED> (A/B knob)
+bool use_ru7() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_RU7");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+int num_cus_conv() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
 }  // namespace
+
+int permute_k1_weight(const bf16_t *w, bf16_t *wp, int n_rows, hipStream_t s) {
+    permute_k1_kernel<<<(n_rows * 128 + 255) / 256, 256, 0, s>>>(w, wp, n_rows);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
     if (a.M <= 0) return 0;
@@ -764,6 +1089,16 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
     const ConvArgs &a = u.c1;
     if (a.Cin != 128 || a.N != 128 || a.taps != 7 || !a.zero || !a.bias || !a.sa) return fail(-1, "resunit128: args");
     if (u.x == u.out_s || a.in == u.out_s) return fail(-1, "resunit128: out_s must not alias x / x_s");
+    if (use_ru7() && u.W2p && u.in_zero_pad && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
+        const int64_t nt = (a.M + ru::BM - 1) / ru::BM;
+        const int nb = (int)std::min<int64_t>(nt, 2 * (int64_t)num_cus_conv());
+        // the k=7 halo past the end reads kActPadRows zero rows behind the input
+        HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * 128), 0, (size_t)kActPadRows * 256, s));
+        if (u.keep_raw) ru7_kernel<true><<<nb, 256, 0, s>>>(u, nt);
+        else ru7_kernel<false><<<nb, 256, 0, s>>>(u, nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (use_conv7() && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
         const int64_t t7 = (a.M + CONV7_BM - 1) / CONV7_BM;
         if (u.keep_raw) conv7_kernel<CONV7_BM, true, true><<<(unsigned)t7, CONV7_BM * 2, 0, s>>>(a, u);

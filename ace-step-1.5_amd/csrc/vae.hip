@@ -38,6 +38,7 @@ struct SnakeP {
 struct ResU {
     SnakeP s1, s2;
     ConvL c1, c2;
+    bf16_t *W2p = nullptr;   // C = 128: c2 weights permuted for ru7_kernel
     int dil = 1;
 };
 struct DecBlk {
@@ -139,7 +140,13 @@ int make_res(acehip_vae *h, const std::string &p, int C, int dil, ResU &r) {
     if ((rc = make_snake(h, p + ".snake1", C, r.s1))) return rc;
     if ((rc = make_snake(h, p + ".snake2", C, r.s2))) return rc;
     if ((rc = make_conv(h, p + ".conv1", C, C, 7, 1, false, true, r.c1))) return rc;
-    return make_conv(h, p + ".conv2", C, C, 1, 1, false, true, r.c2);
+    if ((rc = make_conv(h, p + ".conv2", C, C, 1, 1, false, true, r.c2))) return rc;
+    if (C == 128) {
+        r.W2p = (bf16_t *)valloc(h, (size_t)C * C * 2);
+        if (!r.W2p) return fail(ACEHIP_E_OOM, "vae_finalize: oom");
+        return permute_k1_weight(r.c2.Wp, r.W2p, C, 0);
+    }
+    return 0;
 }
 
 // one implicit-GEMM conv launch
@@ -171,7 +178,8 @@ int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, co
         a.sa = r.s2.a; a.sib = r.s2.ib; a.L_out = L; a.N = 128; a.M = L;
         a.taps = 7; a.dil = r.dil; a.a_stride = 1; a.a_off = -3 * r.dil; a.c_stride = 1; a.c_off = 0;
         a.zero = g_zero_page;
-        u.W2 = r.c2.Wp; u.b2 = r.c2.bias; u.x = X; u.out_s = other;
+        u.W2 = r.c2.Wp; u.W2p = r.W2p; u.b2 = r.c2.bias; u.x = X; u.out_s = other;
+        u.in_zero_pad = 1;   // cur is h->P or h->Q
         u.sa_next = next.a; u.sib_next = next.ib; u.keep_raw = keep_raw ? 1 : 0;
         if ((rc = resunit128(u, s))) return rc;
         // the snaked output is in `other`: copy-free hand-back by swapping roles is done by the caller
@@ -232,9 +240,18 @@ int acehip_vae_create(int device, const acehip_vae_cfg *cfg, acehip_vae **out) {
         }
     }
     h->buf_elems = mx;
-    h->X = (bf16_t *)valloc(h, (size_t)mx * 2);
-    h->P = (bf16_t *)valloc(h, (size_t)mx * 2);
-    h->Q = (bf16_t *)valloc(h, (size_t)mx * 2);
+    // each activation buffer carries kActPadRows zero rows (at the widest stage's row pitch) in
+    // front and as many addressable rows behind: the persistent residual-unit kernel reads its
+    // halo rows before the start from the front ones and whole windows past the end from the
+    // back ones (resunit128 zeroes the first kActPadRows rows past L before each launch)
+    const size_t pad = (size_t)kActPadRows * std::max(h->dec[0].cin, cfg->encoder_hidden * cm[n]) * 2;
+    static_assert(kActPadRows * 2048 * 2 >= 192 * 128 * 2, "back pad covers a C = 128 window");
+    bf16_t **bufs[3] = {&h->X, &h->P, &h->Q};
+    for (bf16_t **b : bufs) {
+        char *p = (char *)valloc(h, (size_t)mx * 2 + 2 * pad);
+        if (p && hipMemset(p, 0, pad) != hipSuccess) p = nullptr;
+        *b = p ? (bf16_t *)(p + pad) : nullptr;
+    }
     h->zero = (bf16_t *)valloc(h, 4096);
     if (h->zero && hipMemset(h->zero, 0, 4096) != hipSuccess) h->zero = nullptr;
     if (!h->X || !h->P || !h->Q || !h->zero) {
