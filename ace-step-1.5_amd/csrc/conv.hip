@@ -167,6 +167,243 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent implicit-GEMM conv for the ConvTranspose phases, the k = 1 convs at C ≥ 256
+// and the encoder's strided convs.  conv_gemm_kernel stages one K-tile ahead on a 2-slot
+// ring, waits vmcnt(0) every K-tile and starts every tile with the operand latency
+// exposed; with 4–32 K-tiles per tile those launches ran at ≈ 40 % of the HBM roof.
+// Here one block per CU (8 waves, 64×32 wave tiles) walks a contiguous range of work
+// items (M-tile, N-tile, phase; phase fastest, then N, so consecutive items share the A
+// panel in L2 — phases as the slowest index sent every ConvTranspose input through HBM
+// once per phase)
+// and the K-tiles of consecutive items form ONE stream through an NS-stage ring
+// (NS = 4, or 3 with a residual): NS − 1 stages are in flight, so the next item's
+// operands land during the current item's epilogue.
+// All loads are LDS-DMA by inline asm with explicit counted waits (hipcc, seeing no
+// vector loads in the loop, inserts no waits of its own — with the builtin DMA it placed
+// vmcnt(0) at every loop merge): the operand stages, the item's residual tile (issued at
+// its first K-step into a swizzled 32 KiB image) and, once per block, the bias / Snake
+// parameters of all N columns.  vmcnt per wave at K-step g (stage g issued at g − NS + 1):
+// younger are the ≤ NS − 2 newer stages, the residual pieces if the item began at a step
+// after stage g was issued, and the previous epilogue's stores if they followed it
+// (partial tiles, whose store count varies, are left out: a safe over-wait).
+namespace cp {
+constexpr int BM = 128, BN = 128, STAGE = (BM + BN) * 128, NW = 8;
+constexpr int PW = (BM + BN) / 8 / NW;                    // operand pieces per wave per stage
+constexpr int RW = BM * 256 / 1024 / NW;                  // residual pieces per wave per item
+constexpr int WM = 2, WN = 4, TM = BM / WM, TN = BN / WN, SM = TM / 16, SN = TN / 16;   // 64×32
+constexpr int MAXN = 1024;                                // parameter image: N ≤ 1024 columns
+constexpr int PAR = MAXN * 10;                            // bias bf16 | sa f32 | sib f32
+}  // namespace cp
+
+__device__ __forceinline__ void cp_dma_v(const void *src, uint32_t lds_addr) {   // 64-bit per-lane address
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(src)
+                 : "memory");
+}
+__device__ __forceinline__ const void *cp_uniform(const void *p) {   // pointer known wave-uniform → SGPRs
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void *)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void cp_dma_s(const void *base, uint32_t voff, uint32_t lds_addr) {   // saddr form
+    base = cp_uniform(base);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff), "s"(base)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void cp_wait() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+template <bool RES, bool RAW, bool SN>
+__global__ __launch_bounds__(512, 1) void convp_kernel(ConvArgs a, int64_t nitems, int phases) {
+    constexpr int CBM = cp::BM, CBN = cp::BN, STG = cp::STAGE, PW = cp::PW, RW = RES ? cp::RW : 0;
+    constexpr int NS = RES ? 3 : 4;
+    constexpr int SM = cp::SM, SNT = cp::SN, TM = cp::TM, TN = cp::TN;
+    constexpr int KST = ((RAW ? 1 : 0) + (SN ? 1 : 0)) * SM;   // epilogue stores per wave per item
+    constexpr int RESB = RES ? CBM * 256 : 0;
+    __shared__ __attribute__((aligned(16))) char lds[cp::PAR + NS * STG + RESB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / cp::WN, wn = wave % cp::WN;
+    const int fr = lane & 15, fc = lane >> 4;
+    const bool odd = fc & 1;
+    const int64_t i0 = nitems * blockIdx.x / gridDim.x, i1 = nitems * (blockIdx.x + 1) / gridDim.x;
+    if (i0 >= i1) return;
+    const int K = a.taps * a.Cin, nk = K / BK;
+    const int64_t G = (i1 - i0) * nk;
+    const int tilesN = a.N / CBN;
+    // parameters of all N columns → LDS (plain loads, retired before the first DMA)
+    bf16_t *pbias = (bf16_t *)lds;
+    float *psa = (float *)(lds + cp::MAXN * 2), *psib = psa + cp::MAXN;
+    for (int c = tid; c < a.N; c += 512) {
+        pbias[c] = a.bias ? a.bias[c] : (bf16_t)0;
+        if constexpr (SN) { psa[c] = a.sa[c]; psib[c] = a.sib[c]; }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    const uint32_t l0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds;
+    const uint32_t lst = l0 + cp::PAR, lres = lst + NS * STG;
+    const char *stb = lds + cp::PAR, *resb = stb + NS * STG;
+
+    // staging cursor (block-uniform): item (phase, m0, n0) and K-tile of the next stage
+    int s_kt = 0, s_phase, s_n0;
+    int64_t s_m0;
+    {
+        s_phase = (int)(i0 % phases);
+        const int64_t w = i0 / phases;
+        s_m0 = (w / tilesN) * CBM;
+        s_n0 = (int)(w % tilesN) * CBN;
+    }
+    int s_slot = 0;            // ring slot of the next stage (rotating: no 64-bit modulo per step)
+    // the lane's W row offset inside a piece (8 rows of 128 B, source-swizzled chunk)
+    const int r8 = lane >> 3;
+    auto stage = [&] {
+        const int k0 = s_kt * BK, tap = k0 / a.Cin, ci0 = k0 - tap * a.Cin;
+        const uint32_t dst = lst + (uint32_t)s_slot * STG;
+#pragma unroll
+        for (int i = 0; i < PW / 2; ++i) {                  // A: im2col rows (zero page outside)
+            const int q = wave + cp::NW * i, r = q * 8 + r8;
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            cp_dma_v(a_src(a, s_m0 + r, tap, ci0, c), dst + q * 1024);
+        }
+        const char *wb = (const char *)(a.W + (int64_t)s_phase * a.w_pstride + (int64_t)s_n0 * K + k0);
+#pragma unroll
+        for (int i = PW / 2; i < PW; ++i) {                 // W rows
+            const int q = wave + cp::NW * i, r = q * 8 + r8 - CBM;
+            const int c = (lane & 7) ^ (((r + CBM) >> 1) & 7);
+            cp_dma_s(wb, (uint32_t)(r * K + c * 8) * 2, dst + q * 1024);
+        }
+        if (++s_slot == NS) s_slot = 0;
+        if (++s_kt == nk) {
+            s_kt = 0;
+            if (++s_phase == phases) {
+                s_phase = 0;
+                s_n0 += CBN;
+                if (s_n0 == a.N) { s_n0 = 0; s_m0 += CBM; }
+            }
+        }
+    };
+    // the item's residual tile: 4 rows × 256 B per piece, chunk c of row r stored at c ^ (r & 15)
+    auto stage_res = [&](int64_t m0, int n0, int phase) {
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+            const int q = wave + cp::NW * i, r = q * 4 + (lane >> 4);
+            const int c = (lane & 15) ^ (r & 15);
+            const int64_t m = min(m0 + r, a.M - 1);
+            const int64_t row = min(max(m * a.c_stride + a.c_off + phase, (int64_t)0), a.L_out - 1);
+            cp_dma_v(a.res + row * a.N + n0 + c * 8, lres + q * 1024);
+        }
+    };
+
+    f32x4 acc[SM][SNT];
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < G) stage();
+    // compute cursor
+    int kt = 0, phase = 0, n0 = 0;
+    int64_t m0 = 0;
+    {
+        phase = (int)(i0 % phases);
+        const int64_t w = i0 / phases;
+        m0 = (w / tilesN) * CBM;
+        n0 = (int)(w % tilesN) * CBN;
+    }
+    bool prev_st = false;      // previous epilogue issued exactly KST stores per wave
+    int slot = 0;
+    for (int64_t g = 0; g < G; ++g) {
+        const int64_t left = G - 1 - g;   // K-steps after this one
+        const int newer = left < NS - 2 ? (int)left : NS - 2;
+        // residual pieces (issued at this item's first step, before that step's refill) are
+        // younger than stage g when g ≥ item start + 1 and stage g was issued at or before it
+        const bool rs = RES && kt >= 1 && kt <= NS - 2;
+        const bool st = prev_st && kt <= NS - 2;
+        const int extra = (rs ? RW : 0) + (st ? KST : 0);
+#define CP_W(E)                                                    \
+    do {                                                           \
+        if (newer == 2) cp_wait<2 * PW + (E)>();                   \
+        else if (newer == 1) cp_wait<PW + (E)>();                  \
+        else cp_wait<(E)>();                                       \
+    } while (0)
+        if (extra == RW + KST) CP_W(RW + KST);
+        else if (extra == KST) CP_W(KST);
+        else if (extra == RW) CP_W(RW);
+        else CP_W(0);
+#undef CP_W
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (RES && kt == 0) stage_res(m0, n0, phase);
+        if (g + NS - 1 < G) stage();
+        const char *b = stb + slot * STG;
+        if (++slot == NS) slot = 0;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 xf[SM], wf[SNT];
+#pragma unroll
+            for (int i = 0; i < SM; ++i) xf[i] = *(const bf16x8 *)(b + swz(wm * TM + i * 16 + fr, ks * 4 + fc));
+#pragma unroll
+            for (int j = 0; j < SNT; ++j) wf[j] = *(const bf16x8 *)(b + swz(CBM + wn * TN + j * 16 + fr, ks * 4 + fc));
+#pragma unroll
+            for (int i = 0; i < SM; ++i)
+#pragma unroll
+                for (int j = 0; j < SNT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        }
+        if (++kt < nk) continue;
+        // epilogue: the residual image retired (younger: the ≤ NS − 1 stages issued after
+        // stage g, all after it), then visible to every wave
+        if (RES) {
+            const int en = left < NS - 1 ? (int)left : NS - 1;
+            if (en == 2) cp_wait<2 * PW>();
+            else if (en == 1) cp_wait<PW>();
+            else cp_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        const int n = n0 + wn * TN + (odd ? 16 : 0) + (fc >> 1) * 8;
+        float bb[8];
+        unpack8(*(const uint4 *)(pbias + n), bb);
+#pragma unroll
+        for (int i = 0; i < SM; ++i) {
+            float o[8];
+            pair8(acc[i][0], acc[i][1], odd, o);
+            acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int rl = wm * TM + i * 16 + fr;
+            const int64_t m = m0 + rl;
+            const int64_t row = m * a.c_stride + a.c_off + phase;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) o[r] = rbf(o[r] + bb[r]);
+            if constexpr (RES) {
+                float rr[8];
+                const int cl = (n - n0) >> 3;           // 16-B chunk of the item's 128 columns
+                unpack8(*(const uint4 *)(resb + rl * 256 + ((cl ^ (rl & 15)) << 4)), rr);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + o[r]);
+            }
+            float sn[8];
+            if constexpr (SN) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) sn[r] = snake1(o[r], psa[n + r], psib[n + r]);
+            }
+            if (m < a.M && row >= 0 && row < a.L_out) {
+                if constexpr (RAW) *(uint4 *)(a.out + row * a.N + n) = pack8(o);
+                if constexpr (SN) *(uint4 *)(a.out_s + row * a.N + n) = pack8(sn);
+            }
+        }
+        prev_st = m0 + CBM <= a.M && m0 * a.c_stride + a.c_off + phase >= 0 &&
+                  (m0 + CBM - 1) * a.c_stride + a.c_off + phase < a.L_out;
+        kt = 0;
+        if (++phase == phases) {
+            phase = 0;
+            n0 += CBN;
+            if (n0 == a.N) { n0 = 0; m0 += CBM; }
+        }
+    }
+}
+
 // Fused Oobleck residual unit at C = 128 (vae_model.py:62-87):
 //   y_s = snake2(conv7_dil(x_s) + b1)            (kept in LDS, never in HBM)
 //   x'  = x + (W2·y_s + b2);  x'_s = snake_next(x')
@@ -1025,6 +1262,17 @@ bool use_conv7() {
     return v == 1;
 }
 
+// ACEHIP_CONVP=1 runs the remaining convs on the persistent counted-ring convp_kernel
+// (measured neutral, r02: decode 44.39 vs 44.06 ms in-process; VAE GPU tests green with it)
+bool use_convp() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_CONVP");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 // ACEHIP_RU7=0 keeps the C = 128 residual units on conv7_kernel<FUSED> (A/B knob)
 bool use_ru7() {
     static int v = -1;
@@ -1072,6 +1320,20 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
     }
     const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
     if (tiles >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
+    if (use_convp() && a.taps * a.Cin / BK >= 3 && a.N <= cp::MAXN) {   // ≥ 3 K-tiles per item (vmcnt bookkeeping)
+        const int64_t items = tiles * phases;
+        const int nb = (int)std::min<int64_t>(items, num_cus_conv());
+        const bool rs = a.res != nullptr, raw = a.out != nullptr, sn = a.out_s != nullptr;
+#define L(R, W, S) convp_kernel<R, W, S><<<nb, 512, 0, s>>>(a, items, phases)
+        if (rs) {
+            if (raw && sn) L(true, true, true); else if (raw) L(true, true, false); else L(true, false, true);
+        } else {
+            if (raw && sn) L(false, true, true); else if (raw) L(false, true, false); else L(false, false, true);
+        }
+#undef L
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     dim3 grid((unsigned)tiles, phases);
     const bool rs = a.res != nullptr, raw = a.out != nullptr, sn = a.out_s != nullptr;
 #define L(R, W, S) conv_gemm_kernel<R, W, S><<<grid, 256, 0, s>>>(a)
