@@ -432,6 +432,114 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
     return 0;
 }
 
+// ---- unit-level parity hooks (single convs / one residual unit, production kernels) ----
+namespace {
+struct Tmp {   // scratch for the parity hooks, freed on scope exit (after a stream sync)
+    std::vector<void *> p;
+    void *get(size_t bytes) {
+        void *q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        p.push_back(q);
+        return q;
+    }
+    ~Tmp() {
+        for (void *q : p) (void)hipFree(q);
+    }
+};
+const bf16_t *hook_zero_page() {
+    static bf16_t *z = nullptr;
+    if (!z && hipMalloc(&z, 4096) == hipSuccess && hipMemset(z, 0, 4096) != hipSuccess) z = nullptr;
+    return z;
+}
+}  // namespace
+
+int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void *w, const void *bias,
+                    const void *res, int Cout, int k, int stride, int dil, void *out, const void *alpha,
+                    const void *beta, void *out_s, void *stream) {
+    if (!in || !w || (!out && !out_s) || (out_s && (!alpha || !beta))) return fail(ACEHIP_E_ARG, "vae_conv: null argument");
+    if (L_in <= 0 || Cin % 64 || Cout % 128 || kind < 0 || kind > 2 || stride < 1 || dil < 1)
+        return fail(ACEHIP_E_ARG, "vae_conv: Cin % 64, Cout % 128, kind 0..2");
+    if ((kind == 0 && (k % 2 == 0 || stride != 1)) || (kind > 0 && k != 2 * stride) || (kind == 2 && L_in % stride))
+        return fail(ACEHIP_E_ARG, "vae_conv: kernel / stride inconsistent with the kind");
+    hipStream_t s = (hipStream_t)stream;
+    g_zero_page = hook_zero_page();
+    if (!g_zero_page) return fail(ACEHIP_E_OOM, "vae_conv: zero page");
+    Tmp t;
+    ConvL c;
+    c.cin = Cin; c.cout = Cout; c.k = k; c.stride = stride; c.transposed = kind == 1;
+    c.Wp = (bf16_t *)t.get((size_t)Cin * Cout * k * 2);
+    c.bias = (bf16_t *)bias;
+    SnakeP sn;
+    if (out_s) {
+        sn.a = (float *)t.get((size_t)Cout * 4);
+        sn.ib = (float *)t.get((size_t)Cout * 4);
+    }
+    if (!c.Wp || (out_s && (!sn.a || !sn.ib))) return fail(ACEHIP_E_OOM, "vae_conv: oom");
+    int rc;
+    if ((rc = pack_conv_weight((const bf16_t *)w, nullptr, kind == 1 ? Cin : Cout, kind == 1 ? Cout : Cin, k,
+                               kind == 1, stride, c.Wp, s)))
+        return rc;
+    if (out_s && (rc = snake_params((const bf16_t *)alpha, (const bf16_t *)beta, Cout, sn.a, sn.ib, s))) return rc;
+    const SnakeP *snp = out_s ? &sn : nullptr;
+    bf16_t *o = (bf16_t *)out, *os = (bf16_t *)out_s;
+    const bf16_t *x = (const bf16_t *)in, *r = (const bf16_t *)res;
+    const int pad = (stride + 1) / 2;
+    if (kind == 0) rc = run_conv(c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s);
+    else if (kind == 1)
+        rc = run_conv(c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s);
+    else rc = run_conv(c, x, L_in, L_in / stride, k, 1, stride, -pad, 1, 0, L_in / stride, o, os, snp, r, 1, s);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+int acehip_vae_resunit(const void *x, const void *x_s, int64_t L, int C, int dil, const void *w1, const void *b1,
+                       const void *alpha2, const void *beta2, const void *w2, const void *b2, const void *alpha_n,
+                       const void *beta_n, void *x_out, void *xs_out, void *stream) {
+    if (!x || !x_s || !w1 || !b1 || !alpha2 || !beta2 || !w2 || !b2 || !alpha_n || !beta_n || !xs_out)
+        return fail(ACEHIP_E_ARG, "vae_resunit: null argument");
+    if (C != 128 || L <= 0 || dil < 1 || dil > 9) return fail(ACEHIP_E_ARG, "vae_resunit: C = 128, dilation 1..9");
+    hipStream_t s = (hipStream_t)stream;
+    g_zero_page = hook_zero_page();
+    if (!g_zero_page) return fail(ACEHIP_E_OOM, "vae_resunit: zero page");
+    Tmp t;
+    // the decoder's activation layout: kActPadRows zero rows in front, addressable rows behind
+    const size_t rowb = (size_t)C * 2, pad = (size_t)kActPadRows * 2048 * 2;
+    char *xs_pad = (char *)t.get((size_t)L * rowb + 2 * pad);
+    bf16_t *xr = (bf16_t *)t.get((size_t)L * rowb);
+    ResU r;
+    r.dil = dil;
+    r.c1.cin = r.c1.cout = C; r.c1.k = 7;
+    r.c2.cin = r.c2.cout = C; r.c2.k = 1;
+    r.c1.Wp = (bf16_t *)t.get((size_t)C * C * 7 * 2);
+    r.c2.Wp = (bf16_t *)t.get((size_t)C * C * 2);
+    r.W2p = (bf16_t *)t.get((size_t)C * C * 2);
+    r.c1.bias = (bf16_t *)b1;
+    r.c2.bias = (bf16_t *)b2;
+    r.s2.a = (float *)t.get(C * 4); r.s2.ib = (float *)t.get(C * 4);
+    SnakeP nx;
+    nx.a = (float *)t.get(C * 4); nx.ib = (float *)t.get(C * 4);
+    bf16_t *other = (bf16_t *)t.get((size_t)L * rowb);
+    if (!xs_pad || !xr || !r.c1.Wp || !r.c2.Wp || !r.W2p || !r.s2.a || !r.s2.ib || !nx.a || !nx.ib || !other)
+        return fail(ACEHIP_E_OOM, "vae_resunit: oom");
+    bf16_t *cur = (bf16_t *)(xs_pad + pad);
+    HIP_TRY(hipMemsetAsync(xs_pad, 0, pad, s));
+    HIP_TRY(hipMemcpyAsync(cur, x_s, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(xr, x, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));
+    int rc;
+    if ((rc = pack_conv_weight((const bf16_t *)w1, nullptr, C, C, 7, 0, 1, r.c1.Wp, s))) return rc;
+    if ((rc = pack_conv_weight((const bf16_t *)w2, nullptr, C, C, 1, 0, 1, r.c2.Wp, s))) return rc;
+    if ((rc = permute_k1_weight(r.c2.Wp, r.W2p, C, s))) return rc;
+    if ((rc = snake_params((const bf16_t *)alpha2, (const bf16_t *)beta2, C, r.s2.a, r.s2.ib, s))) return rc;
+    if ((rc = snake_params((const bf16_t *)alpha_n, (const bf16_t *)beta_n, C, nx.a, nx.ib, s))) return rc;
+    rc = res_unit(r, L, xr, cur, other, nx, x_out != nullptr, s);
+    if (rc < 0 || rc > 1) return rc;
+    HIP_TRY(hipMemcpyAsync(xs_out, rc == 1 ? other : cur, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));
+    if (x_out) HIP_TRY(hipMemcpyAsync(x_out, xr, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
 int acehip_vae_destroy(acehip_vae *h) {
     if (!h) return 0;
     (void)hipSetDevice(h->device);

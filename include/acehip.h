@@ -270,6 +270,27 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
 
 int acehip_vae_destroy(acehip_vae *h);
 
+/* Unit-level parity hooks (no reference counterpart: the per-conv checks of the
+ * Oobleck layers, acestep/models/mlx/vae_model.py:24-230, against fp32
+ * torch.nn.functional.conv1d / conv_transpose1d).  Both run the production weight
+ * packing and kernel selection on channels-last bf16 tensors and synchronise `stream`.
+ * acehip_vae_conv: kind 0 Conv1d(k, dilation dil, padding dil·(k−1)/2); kind 1
+ * ConvTranspose1d(k = 2s, stride s, padding ⌈s/2⌉) (decoder blocks); kind 2 Conv1d(k = 2s,
+ * stride s, padding ⌈s/2⌉) (encoder blocks).  in [L_in][Cin]; w bf16 in torch layout
+ * ([Cout][Cin][k]; kind 1: [Cin][Cout][k]); bias [Cout] or NULL; res [L_out][Cout] or NULL
+ * (out = bf16(res + bf16(conv + bias))); out [L_out][Cout] or NULL; alpha/beta [Cout]
+ * (Snake1d, log-scale) with out_s = Snake(out) or NULL.  Cin % 64 == 0, Cout % 128 == 0.
+ * acehip_vae_resunit: one C = 128 OobleckResidualUnit (vae_model.py:62-87) as the decoder
+ * runs it: x, x_s = bf16(snake1(x)) [L][128] → x_out = x + conv2(snake2(conv1(x_s))) (or
+ * NULL) and xs_out = bf16(snake_next(x_out)); w1 [128][128][7] (dilation dil ≤ 9), w2
+ * [128][128][1]. */
+int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void *w, const void *bias,
+                    const void *res, int Cout, int k, int stride, int dil, void *out, const void *alpha,
+                    const void *beta, void *out_s, void *stream);
+int acehip_vae_resunit(const void *x, const void *x_s, int64_t L, int C, int dil, const void *w1, const void *b1,
+                       const void *alpha2, const void *beta2, const void *w2, const void *b2, const void *alpha_n,
+                       const void *beta_n, void *x_out, void *xs_out, void *stream);
+
 /* The decode output guard of _decode_generate_music_pred_latents
  * (acestep/core/generation/handler/generate_music_decode.py:190-192):
  * per song, peak = max |wav|; if peak > 1 the song is divided by its peak.
