@@ -991,17 +991,7 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
 
 int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.M <= 0) return 0;
-    if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
-        const int cus = num_cus();
-        const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
-        const int nk = a.K / BK;
-        if (tiles * 2 <= cus && nk >= 8) {
-            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4),
-                                                (splitk_fill() * cus + tiles - 1) / tiles);
-            const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
-            if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s);
-        }
-    }
+    // argument checks shared by every path (split-K included)
     if (a.N % 128 || a.K % BK || a.K <= 0)
         return fail(-1, "gemm: N%128 / K%64 violated (M=" + std::to_string(a.M) + " N=" +
                             std::to_string(a.N) + " K=" + std::to_string(a.K) + ")");
@@ -1013,6 +1003,19 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         if (a.N % 256 || h.S <= 0 || (int64_t)h.B * h.S != a.M || (h.nq + h.nk + h.nv) * 128 != a.N ||
             h.S_dst < h.S || (h.nq && !h.qw) || (h.nk && !h.kw) || (h.cos == nullptr) != (h.sin == nullptr))
             return fail(-1, "gemm: head-post arguments inconsistent with the GEMM shape");
+    }
+    if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
+        const int cus = num_cus();
+        const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
+        const int nk = a.K / BK;
+        if (tiles * 2 <= cus && nk >= 8) {
+            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4),
+                                                (splitk_fill() * cus + tiles - 1) / tiles);
+            const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
+            if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s);
+        }
+    }
+    if (a.epi == EPI_HEADPOST) {
         // the fused epilogue exists for the 192-row tile only; a grid of it that fills at
         // most half the chip (cross-Q of the conditional rows, M = 3000) runs as 128×128
         // tiles into the staging buffer + the standalone head_post kernel instead

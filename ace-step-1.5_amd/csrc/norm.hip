@@ -38,7 +38,7 @@ __device__ __forceinline__ typename VecOf<V>::T packv(const float *f) {
 // vectors are loaded once per wave (re-loaded only when the rows cross a
 // batch boundary).
 template <int V, int NV, int R>
-__global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *__restrict__ x,
+__global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *x,   // not restrict: RowAdd writes it (ra.xw)
                                                           const bf16_t *__restrict__ w,
                                                           const bf16_t *__restrict__ shift,
                                                           const bf16_t *__restrict__ scale,

@@ -536,6 +536,43 @@ def test_cfg_row_dedup_matches_full(gpu_device, monkeypatch):
     rt.close()
 
 
+def test_production_cfg_path_all_shortcuts(gpu_device, monkeypatch):
+    """The production CFG call for one song — Bx = 1, Bc = 2, null condition rows
+    (null_condition_emb.expand, base:1907) with set_uniform_rows(1) — runs the layer-0 row
+    dedup, the closed-form null-row cross-attention and the null-row add fused into the MLP
+    norm together: vs all three off (ACEHIP_DIT_DEDUP=0, ACEHIP_FUSE_ROWADD=0, full
+    cross-attention), and vs the bf16 CPU oracle on the expanded condition."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=4, window=16)
+    W = synth_dit_weights(cfg, seed=8, mode="parity")
+    g = torch.Generator().manual_seed(31)
+    T, Lenc = 301, 45
+    xt = torch.randn(1, T, 64, generator=g).bfloat16()
+    ctx = torch.randn(1, T, 128, generator=g).bfloat16()
+    enc = torch.randn(1, Lenc, cfg.hidden_size, generator=g).bfloat16()
+    null = torch.randn(1, 1, cfg.hidden_size, generator=g).bfloat16()
+    encc = torch.cat([enc, null.expand_as(enc)])
+    t = torch.tensor([0.55], dtype=torch.bfloat16)
+    rt = DiTRuntime(cfg, 0, max_S=256, max_Bc=2, max_Lenc=64)
+    rt.load({k: v.to(gpu_device, torch.bfloat16) for k, v in W.items()})
+    rt.set_condition(encc.to(gpu_device))
+    x_d, c_d, t_d = xt.to(gpu_device), ctx.to(gpu_device), t.float().to(gpu_device)
+    rt.set_uniform_rows(1)
+    fast = rt.forward(x_d, c_d, t_d).float().clone()
+    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
+    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "0")
+    rt.set_uniform_rows(2)                                  # off: full cross-attention for every row
+    full = rt.forward(x_d, c_d, t_d).float()
+    torch.cuda.synchronize()
+    assert rel_l2(fast.cpu(), full.cpu()) < 3e-3
+    Wb = {k: v.bfloat16() for k, v in W.items()}
+    with torch.no_grad():
+        ref = dit_oracle.dit_forward(Wb, cfg, torch.cat([xt, xt]), t.expand(2), t.expand(2), encc,
+                                     torch.cat([ctx, ctx])).float()
+    assert rel_l2(fast.cpu(), ref) <= TOL_REL and cosine(fast.cpu(), ref) >= TOL_COS
+    rt.close()
+
+
 def test_null_row_add_fused_into_norm(gpu_device, monkeypatch):
     """The CFG null rows' constant cross-O output added inside the MLP RMSNorm pass
     (RowAdd) is bit-identical to the separate add_row_bcast launch."""
