@@ -15,13 +15,23 @@ namespace acehip {
 // (d = 8·li, li = lane & 15).  Every lane of the wave must call this (it
 // shuffles); norm == false leaves x unchanged (v heads).  `rope` must be
 // uniform over the wave; w is this lane's 8 norm weights, cs/sn its 8 cos/sin.
+// 16-lane row rotations by DPP (row_ror:n, a VALU move): __shfl_xor compiled to
+// ds_bpermute — 12 LDS round trips per (row, head) unit, 4 of them a dependent chain
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm, const float (&w)[8], bool rope,
                                                const float (&cs)[8], const float (&sn)[8], float eps) {
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    // all-reduce over the 16 lanes of the head: rotations by 8, 4, 2, 1 within the row
+    ss += row_ror<8>(ss);
+    ss += row_ror<4>(ss);
+    ss += row_ror<2>(ss);
+    ss += row_ror<1>(ss);
     if (norm) {
         const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + eps);
 #pragma unroll
@@ -30,7 +40,7 @@ __device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm,
     if (rope) {
         float p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = __shfl_xor(x[j], 8, 64);   // rotate-half partner d ± 64
+        for (int j = 0; j < 8; ++j) p[j] = row_ror<8>(x[j]);   // rotate-half partner d ± 64 (lane ^ 8)
         if (norm) {
             const float sg = li < 8 ? -1.0f : 1.0f;
 #pragma unroll
