@@ -34,6 +34,10 @@
 // Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P).  Online softmax in the exp2 domain;
 // masked scores use a finite power-of-two sentinel (a row whose first tiles are
 // fully masked accumulates garbage that the first real tile's rescale zeroes).
+//
+// attn_pw_kernel (band layers by default, ACEHIP_ATTN_PW): the same math with 64 query
+// rows per wave at one wave per SIMD, O / Q / K in asm-owned AGPRs and the softmax VALU
+// hand-placed between the MFMAs (its header below has the schedule and the A/B numbers).
 #include <type_traits>
 #include "kernels.h"
 
@@ -507,6 +511,542 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         }
 }
 
+// ---------------------------------------------------------------------------
+// attn_pw_kernel helpers.  The kernel owns AGPRs a[0:255] by number (the compiler allocates
+// none: its arch-VGPR demand stays < 256 and it issues no MFMA itself):
+//   a[0:127]    O of sub-blocks A (a0-63) and B (a64-127), d-block dt at +16·dt
+//   a[128:191]  Q of A (a128-159) and B (a160-191), k-step s at +4·s
+//   a[192:255]  K fragments of the current tile (keys 0-31 at a192 + 4s, 32-63 at a224 + 4s)
+// Everything that touches them is inline asm, so hipcc neither counts those LDS / global
+// loads (explicit waits) nor pads their hazards (explicit s_nop, noted where used).
+constexpr int PW_O = 0, PW_Q = 128, PW_K = 192;
+// timing experiments only (wrong results): drop the mid-tile barrier / the ring refill /
+// the exponentials / the row max
+#ifndef PW_PV_NOP
+#define PW_PV_NOP 0        // s_nop 1 before every P·V MFMA (else one pf_fence per sub-block)
+#endif
+#ifndef PW_X_NOBAR
+#define PW_X_NOBAR 0
+#endif
+#ifndef PW_X_NODMA
+#define PW_X_NODMA 0
+#endif
+#ifndef PW_X_NOEXP
+#define PW_X_NOEXP 0
+#endif
+#ifndef PW_X_NOMAX
+#define PW_X_NOMAX 0
+#endif
+#ifndef PW_X_NOPV
+#define PW_X_NOPV 0
+#endif
+#ifndef PW_X_NOQK
+#define PW_X_NOQK 0
+#endif
+#ifndef PW_X_NOVREAD
+#define PW_X_NOVREAD 0
+#endif
+#ifndef PW_X_NOKREAD
+#define PW_X_NOKREAD 0
+#endif
+
+__device__ __forceinline__ s16x4 opaque_s16x4() {
+    s16x4 r;
+    asm volatile("" : "=v"(r));
+    return r;
+}
+// compile-time loop: f(IC<I>{}) for I in [I0, I1)
+template <int I0, int I1, typename F>
+__device__ __forceinline__ void sfor(F &&f) {
+    if constexpr (I0 < I1) {
+        f(std::integral_constant<int, I0>{});
+        sfor<I0 + 1, I1>(f);
+    }
+}
+// opaque redefinition: nothing reading x is scheduled above this point
+template <typename T>
+__device__ __forceinline__ void pin(T &x) { asm volatile("" : "+v"(x)); }
+// single-instruction VALU (no SLP packing into v_pk_* beside the MFMAs, no canonicalising v_max)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vadd(float a, float b) {
+    float r;
+    asm volatile("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vfma(float a, float b, float c) {
+    float r;
+    asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// max / sum of a value over the lane pair (l, l ^ 32) by v_permlane32_swap: the two
+// results hold v[l % 32] and v[32 + l % 32], identical on both lanes of the pair.  asm with
+// a leading s_nop 1: the input may come from an asm VALU whose write hipcc does not see
+// (VALU write → v_permlane read hazard)
+__device__ __forceinline__ f32x2 pair32(float x) {
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return f32x2{a, b};
+}
+__device__ __forceinline__ float pair_max(float x) { const f32x2 p = pair32(x); return vmax(p[0], p[1]); }
+__device__ __forceinline__ float pair_sum(float x) { const f32x2 p = pair32(x); return vadd(p[0], p[1]); }
+// two softmax weights p = 2^(s·c − mn) summed into rs, as one hazard-safe stream: each
+// transcendental result is read one instruction after it is written (trans → VALU read)
+// (two partial sums: no add waits on the previous add)
+__device__ __forceinline__ void exp2_pair(float &s0, float &s1, float c, float nmn, float &r0, float &r1) {
+    asm volatile("v_fma_f32 %0, %0, %4, %5\n\t"
+                 "v_fma_f32 %1, %1, %4, %5\n\t"
+                 "v_exp_f32 %0, %0\n\t"
+                 "v_exp_f32 %1, %1\n\t"
+                 "v_add_f32 %2, %2, %0\n\t"
+                 "v_add_f32 %3, %3, %1"
+                 : "+v"(s0), "+v"(s1), "+v"(r0), "+v"(r1) : "v"(c), "v"(nmn));
+}
+
+// k-step S of Sᵀ = K·Qᵀ into st (VGPRs): K at AGPR KA, Q at AGPR QA; S = 0 starts with C = 0.
+// st is not VALU-readable until the XDL write hazard has passed (callers place readers
+// ≥ 2 MFMAs later or behind xdl_pad)
+template <int S, int KA, int QA>
+__device__ __forceinline__ void pw_qk(f32x16 &st) {
+#if PW_X_NOQK
+    if constexpr (S == 0) asm volatile("" : "=v"(st));
+    return;
+#endif
+    if constexpr (S == 0)
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], 0"
+                     : "=v"(st) : "n"(KA), "n"(KA + 3), "n"(QA), "n"(QA + 3));
+    else
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], %0"
+                     : "+v"(st) : "n"(KA), "n"(KA + 3), "n"(QA), "n"(QA + 3));
+}
+// O (AGPR OA..OA+15) += Vᵀ·Pᵀ; s_nop 1 first: P (and V after a register copy) are VALU
+// results the asm cannot see
+template <int OA>
+__device__ __forceinline__ void pw_pv(const bf16x8 &vf, const bf16x8 &pf) {
+#if PW_X_NOPV
+    asm volatile("" :: "v"(vf), "v"(pf));
+    return;
+#endif
+#if PW_PV_NOP
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                 :: "n"(OA), "n"(OA + 15), "v"(vf), "v"(pf));
+#else
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]" :: "n"(OA), "n"(OA + 15), "v"(vf), "v"(pf));
+#endif
+}
+// P of one sub-block complete (all its bf16 converts above this point) and past the VALU
+// write → MFMA read hazard before its P·V starts
+__device__ __forceinline__ void pf_fence(bf16x8 (&pf)[2][2]) {
+    asm volatile("s_nop 1" : "+v"(pf[0][0]), "+v"(pf[0][1]), "+v"(pf[1][0]), "+v"(pf[1][1]));
+}
+template <int KA, int OFF>
+__device__ __forceinline__ void pw_kread(uint32_t lane_off) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+#if PW_X_NOKREAD
+    return;
+#endif
+    asm volatile("ds_read_b128 a[%c0:%c1], %2 offset:%c3" :: "n"(KA), "n"(KA + 3), "v"(lane_off), "n"(OFF));
+}
+// XDL (8 passes) → VALU read of its result: 12 wait states
+__device__ __forceinline__ void xdl_pad(f32x16 &a, f32x16 &b) { asm volatile("s_nop 7\n\ts_nop 4" : "+v"(a), "+v"(b)); }
+template <int A>
+__device__ __forceinline__ void pw_qload(const bf16_t *p) {
+    asm volatile("global_load_dwordx4 a[%c0:%c1], %2, off" :: "n"(A), "n"(A + 3), "v"(p) : "memory");
+}
+template <int R>
+__device__ __forceinline__ float pw_oread() {
+    float x;
+    asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "n"(R));
+    return x;
+}
+// O block of one sub-block (64 AGPRs) *= a; ends with the v_accvgpr_write → MFMA C-read pad
+template <int R>
+__device__ __forceinline__ void pw_scale1(float a) {
+    float t;
+    asm volatile("v_accvgpr_read_b32 %0, a%c1\n\tv_mul_f32 %0, %0, %2\n\tv_accvgpr_write_b32 a%c1, %0"
+                 : "=&v"(t) : "n"(R), "v"(a));
+}
+template <int OA>
+__device__ __forceinline__ void pw_oscale(float a) {
+    asm volatile("s_nop 1");                       // a may be a fresh transcendental result
+    sfor<0, 64>([&](auto I) __attribute__((always_inline)) { pw_scale1<OA + decltype(I)::value>(a); });
+    asm volatile("s_nop 2");
+}
+
+// ---------------------------------------------------------------------------
+// 64 query rows per wave, one wave per SIMD (full / band / cross of the DiT; GQA pair):
+// workgroup = 4 waves = the two query heads of one KV head × 128 queries (waves 0-1 head
+// 2·kvh, waves 2-3 head 2·kvh + 1), each wave two 32-row sub-blocks A, B that share every
+// K and Vᵀ fragment read (half the LDS read traffic per MFMA of attn_fwd_kernel).  One
+// instruction stream interleaves the two sub-blocks: the softmax VALU of one runs in the
+// gaps of the other's MFMAs (MI355X_MICROARCH "one wave per SIMD": a few single-issue
+// fillers hide per MFMA gap) — attn_fwd_kernel's two waves per SIMD instead run the same
+// phase between barriers.  Same work units, tail split, LDS image, swapped Sᵀ = K·Qᵀ
+// layout and lazy rescale as attn_fwd_kernel.
+__global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restrict__ q, const bf16_t *__restrict__ k,
+                                                         const bf16_t *__restrict__ v, bf16_t *__restrict__ o,
+                                                         int H, int KV, int Sq, int Sk, int window, float sl2,
+                                                         int64_t o_ld, SplitArgs sp) {
+    constexpr int NBUF = 2, TILE = KT * 256;
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];
+    // wave index provably uniform (readfirstlane), so every per-wave tile decision below is a
+    // scalar branch (a divergent-looking one makes hipcc structurize both tile variants into
+    // one exec-masked sequence with both register sets live)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    int u = blockIdx.x, part = 0, nsplit = 1;
+    if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
+    if (u >= sp.full) {
+        const int j = u - sp.full;
+        u = sp.full + j / sp.nsplit;
+        part = j % sp.nsplit;
+        nsplit = sp.nsplit;
+    }
+    const int qb = u % sp.nq, kvh = (u / sp.nq) % KV, b = u / (sp.nq * KV);
+    const int hq = 2 * kvh + (wave >> 1);
+    const int qblk = qb * QB;
+    const int q0 = qblk + (wave & 1) * 64;     // this wave's 64 rows: sub-block sb = rows q0 + 32·sb + r
+    const int qi[2] = {q0 + r, q0 + 32 + r};
+
+    // O = 0 and Q → AGPRs (the clobber of a0 / a255 makes the kernel descriptor allocate all 256)
+    sfor<0, 128>([&](auto I) __attribute__((always_inline)) {
+        asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "n"(PW_O + decltype(I)::value));
+    });
+    asm volatile("s_nop 0" ::: "a0", "a255");
+    sfor<0, 2>([&](auto SB) __attribute__((always_inline)) {
+        constexpr int sb = decltype(SB)::value;
+        const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi[sb], Sq - 1)) * 128 + 8 * hh;
+        sfor<0, 8>([&](auto S) __attribute__((always_inline)) {
+            pw_qload<PW_Q + 32 * sb + 4 * decltype(S)::value>(qp + 16 * decltype(S)::value);
+        });
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    int kv_lo = 0, kv_hi = Sk;
+    if (window >= 0) {
+        kv_lo = max(0, qblk - window);
+        kv_hi = min(Sk, qblk + QB + window);
+    }
+    int t_first = kv_lo / KT;
+    int ntiles = (kv_hi + KT - 1) / KT - t_first;
+    if (nsplit > 1) {
+        const int per = (ntiles + nsplit - 1) / nsplit;
+        const int t0 = min(ntiles, part * per), t1 = min(ntiles, t0 + per);
+        t_first += t0;
+        ntiles = t1 - t0;
+    }
+    // 32 KiB tile = 32 LDS-DMA wave-instructions, 8 per wave
+    auto stage_tile = [&](int kv0, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = wave * 8 + i;
+            const int isv = c >> 4, row = (c & 15) * 4 + (lane >> 4), pc = lane & 15;
+            const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+            const int key = min(kv0 + row, Sk - 1);
+            glds16((isv ? vp : kp) + (int64_t)key * 128 + ch * 8, lds + (isv * NBUF + buf) * TILE + (c & 15) * 1024);
+        }
+    };
+
+    const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    uint32_t koff[8], voff[4][2];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) koff[s] = lds_base + kvoff(r, 2 * s + hh);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int h8 = 0; h8 < 2; ++h8)
+            voff[dt][h8] = lds_base + NBUF * TILE +
+                           kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+
+    float m[2] = {NEG, NEG}, l[2] = {0.f, 0.f};
+    // K read i (0..15) of ring slot SLOT into the K AGPRs
+    auto k_read = [&](auto SLOTC, auto IC_) __attribute__((always_inline)) {
+        constexpr int KB = decltype(SLOTC)::value * TILE, i = decltype(IC_)::value;
+        pw_kread<PW_K + 4 * i, KB + (i >> 3) * 32 * 256>(koff[i & 7]);
+    };
+    auto tile_barrier = [&] __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    // Per tile it (ring slot SLOT; K(it) already read into a[192:255], DMA(it+1) in flight):
+    //   1  QKᵀ of A (16 MFMAs)       ∥ the tile's 32 Vᵀ reads, A's max over key half 0
+    //   2  QKᵀ of B (16 MFMAs)       ∥ A's max over key half 1, A's exponentials
+    //   3  A's last exponentials, P_A, O_A rescale (rare), B's max
+    //      ── own DMA landed + own reads retired, barrier: tile it+1 visible, slot SLOT free;
+    //         DMA(it+2) into slot SLOT
+    //   4  P·V of A (16 MFMAs)       ∥ B's exponentials
+    //   5  P_B, O_B rescale (rare); P·V of B (16 MFMAs) ∥ K(it+1) reads
+    // A wave whose 64 rows have no key of the tile in their band skips the compute (barrier,
+    // DMA and the next K reads stay).
+    auto tile = [&](int it, auto SLOTC, auto MASKC, bool outside) __attribute__((always_inline)) {
+        constexpr int SLOT = decltype(SLOTC)::value;
+        constexpr int NSLOT = (SLOT + 1) % NBUF;
+        const int kv0 = (t_first + it) * KT;
+        s16x4 rv[4][2][2][2];         // Vᵀ fragments of the current tile, per d-block
+        f32x16 st[2][2];              // scores per sub-block and key half
+        bf16x8 pf[2][2][2];           // P (bf16) per sub-block, B operand of P·V
+        float mx[2], mx2[2], mn[2], alpha[2], rs[2], rs2[2];
+
+        // Vᵀ read i (0..31) of ring slot SLOT
+        auto v_read = [&](auto SLOTC, auto IC_) __attribute__((always_inline)) {
+            constexpr int VB = decltype(SLOTC)::value * TILE, i = decltype(IC_)::value;
+            constexpr int dt = i >> 3, t = (i >> 2) & 1, s = (i >> 1) & 1, h8 = i & 1;
+#if PW_X_NOVREAD
+            rv[dt][t][s][h8] = opaque_s16x4();
+#else
+            rv[dt][t][s][h8] = ds_read_tr16_imm<VB + (32 * t + 16 * s) * 256>(voff[dt][h8]);
+#endif
+        };
+        auto v_wait = [&] __attribute__((always_inline)) {
+    #pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(rv[dt][0][0][0]), "+v"(rv[dt][0][0][1]), "+v"(rv[dt][0][1][0]), "+v"(rv[dt][0][1][1]),
+                               "+v"(rv[dt][1][0][0]), "+v"(rv[dt][1][0][1]), "+v"(rv[dt][1][1][0]), "+v"(rv[dt][1][1][1]));
+        };
+        // MFMA gg (0..15) of the Sᵀ products of sub-block SB: key half gg / 8, k-step gg % 8
+        auto qk_mfma = [&](auto SBC, auto GC) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value, gg = decltype(GC)::value;
+            constexpr int t = gg >> 3, s = gg & 7;
+            pw_qk<s, PW_K + 32 * t + 4 * s, PW_Q + 32 * sb + 4 * s>(st[sb][t]);
+        };
+        // MFMA gg (0..15) of P·V of sub-block SB: d-block gg / 4, (key half, k-step) gg % 4
+        auto pv_mfma = [&](auto SBC, auto GC) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value, gg = decltype(GC)::value;
+            constexpr int dt = gg >> 2, t = (gg >> 1) & 1, s = gg & 1;
+            const s16x8 cat = __builtin_shufflevector(rv[dt][t][s][0], rv[dt][t][s][1], 0, 1, 2, 3, 4, 5, 6, 7);
+            pw_pv<PW_O + 64 * sb + 16 * dt>(__builtin_bit_cast(bf16x8, cat), pf[sb][t][s]);
+        };
+        // Softmax pieces.  Each opens with pin() of what it reads: an opaque redefinition after
+        // the MFMA issued just before it, so hipcc cannot hoist the piece above that MFMA (it
+        // would otherwise gather all VALU ahead of the MFMA stream); its running result feeds the
+        // next piece's pin, so it cannot sink far either.
+        // max over scores j0 .. j0+7 of key half T (the band / Sk mask first when MASK)
+        auto max_piece = [&](auto SBC, auto TC, auto J0C, auto MASKC, int kv0) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value, t = decltype(TC)::value, j0 = decltype(J0C)::value;
+            pin(mx[sb]);
+            pin(mx2[sb]);
+            if constexpr (decltype(MASKC)::value) {
+                // key kv0 + c (c = 32t + (j&3) + 8(j>>2) + 4hh) is admissible iff c ∈ [lo, hi]
+                const int lo = (window >= 0 ? qi[sb] - window : -0x40000000) - kv0 - 4 * hh;
+                const int hi = min(window >= 0 ? qi[sb] + window : 0x3fffffff, Sk - 1) - kv0 - 4 * hh;
+                const uint32_t span = hi >= lo ? (uint32_t)(hi - lo) : 0u;
+                const bool none = hi < lo;
+    #pragma unroll
+                for (int j = j0; j < j0 + 8; ++j) {
+                    const int c = 32 * t + (j & 3) + 8 * (j >> 2);
+                    const bool ok = !none & ((uint32_t)(c - lo) <= span);
+                    st[sb][t][j] = ok ? st[sb][t][j] : NEG;
+                }
+            }
+    #pragma unroll
+            for (int j = j0; j < j0 + 8; j += 4) {
+#if !PW_X_NOMAX
+            mx[sb] = vmax3(mx[sb], st[sb][t][j], st[sb][t][j + 1]);
+            mx2[sb] = vmax3(mx2[sb], st[sb][t][j + 2], st[sb][t][j + 3]);
+#endif
+        }
+        };
+        // row max over the lane pair, the lazy-rescale reference max and its factor
+        auto max_finish = [&](auto SBC) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value;
+            pin(mx[sb]);
+            pin(mx2[sb]);
+            const float x = pair_max(vmax(mx[sb], mx2[sb])) * sl2;
+            mn[sb] = x > m[sb] + ATT_TAU ? x : m[sb];
+            alpha[sb] = __builtin_amdgcn_exp2f(m[sb] - mn[sb]);
+            m[sb] = mn[sb];
+            rs[sb] = 0.f;
+            rs2[sb] = 0.f;
+        };
+        // P = 2^(s·sl2 − mn) of scores j0, j0+1 of key half T, summed into rs
+        auto exp_piece = [&](auto SBC, auto TC, auto J0C) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value, t = decltype(TC)::value, j0 = decltype(J0C)::value;
+            pin(rs[sb]);
+            pin(rs2[sb]);
+            float s0 = st[sb][t][j0], s1 = st[sb][t][j0 + 1];
+#if !PW_X_NOEXP
+            exp2_pair(s0, s1, sl2, -mn[sb], rs[sb], rs2[sb]);
+#endif
+            st[sb][t][j0] = s0;
+            st[sb][t][j0 + 1] = s1;
+        };
+        // row sum over the lane pair, l, P → bf16, and the (rare) O rescale
+        auto exp_finish = [&](auto SBC) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SBC)::value;
+            pin(rs[sb]);
+            pin(rs2[sb]);
+            l[sb] = l[sb] * alpha[sb] + pair_sum(vadd(rs[sb], rs2[sb]));
+    #pragma unroll
+            for (int t = 0; t < 2; ++t)
+    #pragma unroll
+                for (int s = 0; s < 2; ++s)
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) pf[sb][t][s][j] = (__bf16)st[sb][t][8 * s + j];
+            if (__any(alpha[sb] != 1.0f)) pw_oscale<PW_O + 64 * sb>(alpha[sb]);
+        };
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // K(it) in a[192:255]
+        if (!outside) {
+            mx[0] = mx[1] = mx2[0] = mx2[1] = NEG;
+            sfor<0, 16>([&](auto G) __attribute__((always_inline)) {     // phase 1
+                constexpr int gg = decltype(G)::value;
+                qk_mfma(IC<0>{}, G);
+                v_read(SLOTC, IC<2 * gg>{});
+                v_read(SLOTC, IC<2 * gg + 1>{});
+                if constexpr (gg >= 10 && gg < 12) max_piece(IC<0>{}, IC<0>{}, IC<8 * (gg - 10)>{}, MASKC, kv0);
+            });
+            sfor<0, 16>([&](auto G) __attribute__((always_inline)) {     // phase 2
+                constexpr int gg = decltype(G)::value;
+                qk_mfma(IC<1>{}, G);
+                if constexpr (gg >= 2 && gg < 4) max_piece(IC<0>{}, IC<1>{}, IC<8 * (gg - 2)>{}, MASKC, kv0);
+                if constexpr (gg == 4) max_finish(IC<0>{});
+                if constexpr (gg >= 5) exp_piece(IC<0>{}, IC<((gg - 5) >> 3)>{}, IC<(2 * ((gg - 5) & 7))>{});
+            });
+            // phase 3: A's exponentials of key half 1, j = 6..15
+            sfor<0, 5>([&](auto G) __attribute__((always_inline)) {
+                exp_piece(IC<0>{}, IC<1>{}, IC<(6 + 2 * decltype(G)::value)>{});
+            });
+            exp_finish(IC<0>{});
+            xdl_pad(st[1][0], st[1][1]);           // B's QKᵀ chain just ended
+            max_piece(IC<1>{}, IC<0>{}, IC<0>{}, MASKC, kv0);
+            max_piece(IC<1>{}, IC<0>{}, IC<8>{}, MASKC, kv0);
+            max_piece(IC<1>{}, IC<1>{}, IC<0>{}, MASKC, kv0);
+            max_piece(IC<1>{}, IC<1>{}, IC<8>{}, MASKC, kv0);
+            max_finish(IC<1>{});
+            v_wait();
+        }
+#if !PW_X_NOBAR
+        tile_barrier();
+#endif
+#if !PW_X_NODMA
+        if (it + 2 < ntiles) stage_tile(kv0 + 2 * KT, SLOT);
+#endif
+        const bool more = it + 1 < ntiles;
+        if (!outside) {
+            pf_fence(pf[0]);
+            sfor<0, 16>([&](auto G) __attribute__((always_inline)) {     // phase 4
+                constexpr int gg = decltype(G)::value;
+                pv_mfma(IC<0>{}, G);
+                exp_piece(IC<1>{}, IC<(gg >> 3)>{}, IC<(2 * (gg & 7))>{});
+            });
+            exp_finish(IC<1>{});
+            pf_fence(pf[1]);
+            if (more) {
+                sfor<0, 16>([&](auto G) __attribute__((always_inline)) {  // phase 5
+                    pv_mfma(IC<1>{}, G);
+                    k_read(IC<NSLOT>{}, G);
+                });
+            } else {
+                sfor<0, 16>([&](auto G) __attribute__((always_inline)) { pv_mfma(IC<1>{}, G); });
+            }
+        } else if (more) {
+            sfor<0, 16>([&](auto G) __attribute__((always_inline)) { k_read(IC<NSLOT>{}, G); });
+        }
+    };
+    // band: tiles outside the band of all 64 rows skipped; tiles inside it for all 64 mask-free
+    auto run_tile = [&](int it, auto SLOTC) __attribute__((always_inline)) {
+        const int kv0 = (t_first + it) * KT;
+        const bool outside = window >= 0 && (kv0 > q0 + 63 + window || kv0 + KT - 1 < q0 - window);
+        const bool interior = kv0 + KT <= Sk && (window < 0 || (kv0 >= q0 + 63 - window && kv0 + KT - 1 <= q0 + window));
+        if (interior) tile(it, SLOTC, IC<0>{}, outside);
+        else tile(it, SLOTC, IC<1>{}, outside);
+    };
+    // prologue: tile 0 staged and visible, tile 1 in flight, K(0) read
+    if (ntiles > 0) stage_tile(t_first * KT, 0);
+    tile_barrier();
+    if (ntiles > 1) stage_tile((t_first + 1) * KT, 1);
+    if (ntiles > 0) sfor<0, 16>([&](auto G) __attribute__((always_inline)) { k_read(IC<0>{}, G); });
+    int it = 0;
+    for (; it + 1 < ntiles; it += 2) {
+        run_tile(it, IC<0>{});
+        run_tile(it + 1, IC<1>{});
+    }
+    if (it < ntiles) run_tile(it, IC<0>{});
+
+    // O out of the AGPRs (the last MFMAs wrote them just before: XDL → read pad)
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+    f32x16 oacc[2][4];
+    sfor<0, 128>([&](auto I) __attribute__((always_inline)) {
+        constexpr int i = decltype(I)::value;
+        oacc[i >> 6][(i >> 4) & 3][i & 15] = pw_oread<PW_O + i>();
+    });
+
+    if (nsplit > 1) {
+        // tail-split hand-off as in attn_fwd_kernel; "sub-wave" index 2·wave + sb
+        const int64_t wsz = 66 * 64;
+        auto st_c = [](float *p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        auto ld_c = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+            float *mine = sp.ws + (((int64_t)(u - sp.full) * nsplit + part) * 8 + 2 * wave + sb) * wsz;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) st_c(mine + (16 * i + j) * 64 + lane, oacc[sb][i][j]);
+            st_c(mine + 64 * 64 + lane, m[sb]);
+            st_c(mine + 65 * 64 + lane, l[sb]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ int s_ticket;
+        if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
+        __syncthreads();
+        if (s_ticket != nsplit - 1) return;
+        for (int p2 = 0; p2 < nsplit; ++p2) {
+            if (p2 == part) continue;
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb) {
+                const float *oth = sp.ws + (((int64_t)(u - sp.full) * nsplit + p2) * 8 + 2 * wave + sb) * wsz;
+                const float m2 = ld_c(oth + 64 * 64 + lane), l2 = ld_c(oth + 65 * 64 + lane);
+                const float mm = fmaxf(m[sb], m2);
+                const float a1 = __builtin_amdgcn_exp2f(m[sb] - mm), a2 = __builtin_amdgcn_exp2f(m2 - mm);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j)
+                        oacc[sb][i][j] = oacc[sb][i][j] * a1 + ld_c(oth + (16 * i + j) * 64 + lane) * a2;
+                l[sb] = l[sb] * a1 + l2 * a2;
+                m[sb] = mm;
+            }
+        }
+        if (tid == 0) sp.cnt[u - sp.full] = 0;
+    }
+
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+        if (qi[sb] >= Sq) continue;            // both lanes of a row pair leave together
+        const float inv = 1.0f / l[sb];
+        bf16_t *op = o + ((int64_t)b * Sq + qi[sb]) * o_ld + hq * 128;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp) {
+                float vv[8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float a0 = oacc[sb][dt][8 * gp + j] * inv, a1 = oacc[sb][dt][8 * gp + 4 + j] * inv;
+                    const float got = __shfl_xor(hh ? a0 : a1, 32, 64);
+                    vv[j] = hh ? got : a0;
+                    vv[4 + j] = hh ? a1 : got;
+                }
+                *(uint4 *)(op + 32 * dt + 16 * gp + 8 * hh) = pack8(vv);
+            }
+    }
+}
+
 }  // namespace
 
 static int num_cus_attn() {
@@ -547,6 +1087,33 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // SIMD partners run out of phase. Measured (r02, one box): band −3 %, cross −9 %,
     // full (47 tiles: the doubled K/V staging dominates) +7 %, cross with fewer pair units
     // than CUs (B = 1) +11 %, short split-KV cross slower.
+    // 64-row-per-wave kernel for the DiT's unmasked GQA-pair layers: ACEHIP_ATTN_PW = bit mask of
+    // the layer kinds that use it (1 full, 2 band, 4 cross = window < 0 with Sk != Sq).  r02 A/B
+    // (tools/bench_attn.py, one process, three boxes): band 46.4-48.4 vs 47.6-48.8 µs (kept),
+    // full 166-189 vs 161-179 and B = 1 cross 30.5-31.8 vs 29.6-30.6 (stay on attn_fwd_kernel)
+    int pw_mask = 2;
+    if (const char *e = getenv("ACEHIP_ATTN_PW")) pw_mask = atoi(e);
+    const int kind_bit = window >= 0 ? 2 : (Sk == Sq ? 1 : 4);
+    if (grp == 2 && !kmask && window != ATTN_CAUSAL && (pw_mask & kind_bit)) {
+        const int units = nq * KV * B;
+        SplitArgs sp{nq, units, 1, nullptr, nullptr};
+        const int tail = units % cus;
+        if (ws && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
+            sp.full = units - tail;
+            sp.nsplit = min(4, cus / tail);
+        } else if (ws && window < 0 && units * 2 <= cus && unit_tiles >= 4) {
+            sp.full = 0;
+            sp.nsplit = min(min(cus / units, unit_tiles / 2), 16);
+        }
+        if (sp.nsplit > 1) {
+            sp.cnt = (int *)ws;
+            sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
+        }
+        const int grid = sp.full + (units - sp.full) * sp.nsplit;
+        attn_pw_kernel<<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     const bool short_split = window < 0 && nq * KV * B * 2 <= cus && unit_tiles >= 4;
     const bool split_heads = ATT_SPLIT_HEADS && grp == 2 && window != ATTN_CAUSAL &&
                              unit_tiles < 24 && !short_split && nq * KV * B > cus;

@@ -92,7 +92,7 @@ struct acehip_dit {
     bool graph_on = false;
     hipStream_t cap_stream = nullptr;
     hipGraphExec_t gexec = nullptr;
-    int gkey[5] = {-1, -1, -1, -1, -1};
+    int gkey[6] = {-1, -1, -1, -1, -1, -1};
 
     // fp32 parity mode (acehip_dit_cfg.fp32): fp32 weights and workspace,
     // the kernels of f32.hip; the bf16 buffers above are not allocated
@@ -112,6 +112,7 @@ struct acehip_dit {
 };
 
 static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s);
+static int knob_hash();
 static int create_f32(acehip_dit *h);
 static int set_weight_f32(acehip_dit *h, Slot &s, const void *ptr, int dtype, int64_t n, int on_device);
 static int build_rope_f32(acehip_dit *h);
@@ -555,7 +556,7 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     if (!h->graph_on || h->prof) {
         RUN(forward_body(h, Bc, S, dup, s));
     } else {
-        const int key[5] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), dup ? 1 : 0};
+        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), dup ? 1 : 0, knob_hash()};
         if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
             if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
             if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
@@ -590,6 +591,22 @@ int acehip_dit_set_graph(acehip_dit *h, int enable) {
 }
 
 }  // extern "C"
+
+// hash of the A/B environment knobs the captured forward body reads (GEMM / split-K /
+// attention / row-add variants): a change re-captures the graph instead of replaying a
+// stale one
+static int knob_hash() {
+    static const char *const names[] = {"ACEHIP_ATTN_CUS", "ACEHIP_ATTN_PW", "ACEHIP_FUSE_ROWADD",
+                                        "ACEHIP_GEMM_HP128", "ACEHIP_GEMM_TAILSPLIT", "ACEHIP_GEMM_W4",
+                                        "ACEHIP_GEMM_W4S", "ACEHIP_SPLITK_FILL", "ACEHIP_SPLITK_STAGES"};
+    uint32_t h = 2166136261u;                      // FNV-1a over "name=value;" pairs
+    for (const char *n : names) {
+        const char *v = getenv(n);
+        for (const char *c : {n, "=", v ? v : "", ";"})
+            for (; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
+    }
+    return (int)(h & 0x7fffffff);
+}
 
 // Everything of one forward between the input packing and proj_out: reads only handle
 // buffers (emb, Xin, weights, K/V cache), so it can be captured once and replayed.
@@ -811,11 +828,9 @@ int acehip_rmsnorm_bf16(const void *x, const void *w, const void *shift, const v
     if (!x || !w || !out) return fail(ACEHIP_E_ARG, "null argument");
     if (rows_per_wave == 3 || rows_per_wave > 4 || (rows_per_wave < 0 && rows_per_wave != -2 && rows_per_wave != -4))
         return fail(ACEHIP_E_ARG, "rows_per_wave");
-    rmsnorm_set_rows(rows_per_wave);
-    const int rc = rmsnorm_mod((const bf16_t *)x, (const bf16_t *)w, (const bf16_t *)shift, (const bf16_t *)scale,
-                               mod_bstride, rows_per_batch, (bf16_t *)out, M, D, eps, (hipStream_t)stream);
-    rmsnorm_set_rows(0);
-    return rc;
+    return rmsnorm_mod((const bf16_t *)x, (const bf16_t *)w, (const bf16_t *)shift, (const bf16_t *)scale,
+                       mod_bstride, rows_per_batch, (bf16_t *)out, M, D, eps, (hipStream_t)stream, RowAdd{},
+                       rows_per_wave);
 }
 
 int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int B, int S, int nq, int nk,

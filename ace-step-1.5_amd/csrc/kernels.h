@@ -75,7 +75,6 @@ int crop_rows(const bf16_t *src, int Bc, int rows_src, int rows_dst, int C, bf16
 // out[m] = AdaLN or plain RMSNorm of x[m] (rows of D):
 //   plain: bf16(w · bf16(x·rsqrt(mean x²+eps)))
 //   mod:   bf16(bf16(plain · bf16(1+scale[b])) + shift[b])
-void rmsnorm_set_rows(int rows_per_wave);   // 0 = default
 // optional row add fused into rmsnorm_mod: rows >= from first become x = bf16(x + v[D]),
 // written back to xw (== x)
 struct RowAdd {
@@ -83,9 +82,11 @@ struct RowAdd {
     const bf16_t *v = nullptr;
     int from = 0;
 };
+// rows_per_wave: kernel variant (tests / micro-bench: 1, 2, 4 rows per wave, −2 / −4 waves
+// per row); 0 = the default (1)
 int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
-                hipStream_t s, RowAdd ra = RowAdd{});
+                hipStream_t s, RowAdd ra = RowAdd{}, int rows_per_wave = 0);
 int head_post(const HeadPostArgs &a, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---

@@ -233,9 +233,6 @@ __global__ __launch_bounds__(256) void head_post_kernel(HeadPostArgs a) {
 
 }  // namespace
 
-static int g_rms_rows = 0;   // rows per wave override (tests / micro-bench); 0 = default
-void rmsnorm_set_rows(int r) { g_rms_rows = r; }
-
 template <int R>
 static void rms_launch(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                        int64_t mbs, int rpb, bf16_t *out, int M, int D, float eps, RowAdd ra, hipStream_t s) {
@@ -270,13 +267,13 @@ static void rms_launch(const bf16_t *x, const bf16_t *w, const bf16_t *shift, co
 
 int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf16_t *scale,
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
-                hipStream_t s, RowAdd ra) {
+                hipStream_t s, RowAdd ra, int rows_per_wave) {
     if (M <= 0) return 0;
     if (ra.v && (!ra.xw || ra.xw != x)) return fail(-1, "rmsnorm: row add must write back to x");
     if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
     if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
     const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
-    const int R = g_rms_rows ? g_rms_rows : 1;
+    const int R = rows_per_wave ? rows_per_wave : 1;
     if (R < 0 && !ra.v && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
         const int WPR = -R, nv = D / (512 * WPR), grid = (M + 4 / WPR - 1) / (4 / WPR);
 #define SPLIT(NV_, W_) \

@@ -75,11 +75,13 @@ def test_gemm_variants(gpu_device, variant, M, N, K):
 
 
 @pytest.mark.parametrize("cus,window", [(16, -1), (18, -1), (20, -1)])
-def test_attention_tail_split(gpu_device, monkeypatch, cus, window):
+@pytest.mark.parametrize("pw", ["0", "7"])
+def test_attention_tail_split(gpu_device, monkeypatch, cus, window, pw):
     """Tail balancing with 2-, 3- and 4-way KV splits (24 units; CU count 16/18/20 → tail 8/6/4 →
     nsplit 2/3/4; overridden so small
     shapes take the split path): merged partials must match the fp32 reference."""
     monkeypatch.setenv("ACEHIP_ATTN_CUS", str(cus))
+    monkeypatch.setenv("ACEHIP_ATTN_PW", pw)
     ff = _lib()
     B, H, KV, Sq, Sk = 2, 4, 2, 700, 1600       # 6 q-blocks x 2 KV x 2 = 24 units, 25 KV tiles
     g = torch.Generator(device="cpu").manual_seed(cus * 3 + window)
@@ -122,7 +124,11 @@ def _attn_ref(q, k, v, window):
                                                   # causal: text encoder (128 tokens), ragged, nrep 1
                                                   (2, 16, 8, 128, 128, -2), (1, 16, 8, 77, 77, -2),
                                                   (3, 4, 2, 300, 300, -2), (1, 2, 2, 257, 257, -2)])
-def test_attention(gpu_device, B, H, KV, Sq, Sk, window):
+@pytest.mark.parametrize("pw", ["0", "7"])
+def test_attention(gpu_device, monkeypatch, B, H, KV, Sq, Sk, window, pw):
+    """pw: ACEHIP_ATTN_PW — "0" every layer kind on attn_fwd_kernel, "7" the GQA-pair unmasked
+    kinds (full / band / cross) on the 64-row-per-wave attn_pw_kernel (production: band only)."""
+    monkeypatch.setenv("ACEHIP_ATTN_PW", pw)
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(Sq * 7 + Sk)
     q = torch.randn(B, H, Sq, 128, generator=g).to(gpu_device, torch.bfloat16)
