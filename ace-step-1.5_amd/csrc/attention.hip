@@ -1098,7 +1098,9 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         const int units = nq * KV * B;
         SplitArgs sp{nq, units, 1, nullptr, nullptr};
         const int tail = units % cus;
-        if (ws && unit_tiles >= 24 && units > cus && tail > 0 && tail <= cus / 2) {
+        int split_min = 24;        // shortest KV loop (tiles) whose tail units are split over KV ranges
+        if (const char *e = getenv("ACEHIP_ATTN_PW_SPLIT")) split_min = atoi(e);
+        if (ws && unit_tiles >= split_min && units > cus && tail > 0 && tail <= cus / 2) {
             sp.full = units - tail;
             sp.nsplit = min(4, cus / tail);
         } else if (ws && window < 0 && units * 2 <= cus && unit_tiles >= 4) {

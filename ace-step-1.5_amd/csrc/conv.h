@@ -40,7 +40,8 @@ int resunit128(const ResUnitArgs &u, hipStream_t s);
 // layout is the k=1 MFMA's B operand (ru7_kernel): new 8g+e ← old e<4 ? 4g+e : 16+4g+e−4
 int permute_k1_weight(const bf16_t *w, bf16_t *wp, int n_rows, hipStream_t s);
 int conv_gemm(const ConvArgs &a, int phases, hipStream_t s);
-// final decoder conv: snaked NLC [L][Cin] → fp32 channels-first [Cout=2][L], k 7, no bias
+// final decoder conv: snaked NLC [L][Cin] → fp32 channels-first [Cout=2][L], k 7, no bias;
+// w [7][Cin][2] (the two output channels adjacent), Cin = 128
 int conv_out(const bf16_t *in_s, int64_t L, int Cin, const float *w, int Cout, float *out, hipStream_t s);
 // encoder first conv: channels-first [Cin≤2][N] → raw + snaked NLC [N][Cout], k 7, bias
 int conv_in(const bf16_t *in, int64_t N, int Cin, const float *w, const float *bias, int Cout,

@@ -67,7 +67,7 @@ struct acehip_vae {
     ConvL dconv1;
     std::vector<DecBlk> dec;
     SnakeP dsnake;
-    float *dconv2_w = nullptr;  // [2][7][C]
+    float *dconv2_w = nullptr;  // [7][C][2] (output channel innermost)
     // encoder
     float *econv1_w = nullptr, *econv1_b = nullptr;  // [C][2][7], [C]
     std::vector<EncBlk> enc;
@@ -320,6 +320,16 @@ int acehip_vae_finalize(acehip_vae *h) {
         if ((rc = fuse_conv_weight_f32(v->p, g ? g->p : nullptr, c.audio_channels, c.decoder_channels, 7, 1,
                                        h->dconv2_w, 0)))
             return rc;
+        // conv_out reads the two output channels' weights as adjacent pairs [7][C][2]
+        const size_t n = (size_t)c.audio_channels * 7 * c.decoder_channels;
+        std::vector<float> w(n), wp(n);
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(w.data(), h->dconv2_w, n * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n / 2; ++i) {
+            wp[2 * i] = w[i];
+            wp[2 * i + 1] = w[n / 2 + i];
+        }
+        HIP_TRY(hipMemcpy(h->dconv2_w, wp.data(), n * 4, hipMemcpyHostToDevice));
     }
     if (c.with_encoder) {
         Raw *v = find(h, "encoder.conv1.weight_v"), *g = find(h, "encoder.conv1.weight_g");
