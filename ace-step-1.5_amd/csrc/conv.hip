@@ -1267,15 +1267,17 @@ bool use_conv7() {
     return v == 1;
 }
 
-// ACEHIP_CONVP=1 runs the remaining convs on the persistent counted-ring convp_kernel
-// (measured neutral, r02: decode 44.39 vs 44.06 ms in-process; VAE GPU tests green with it)
-bool use_convp() {
+// Which of the remaining convs run on the persistent counted-ring convp_kernel:
+// default the k = 1 convs (C ≥ 256, residual epilogue), ACEHIP_CONVP=1 every eligible conv,
+// =0 none.  Per-kernel rocprof of a 240 s decode (r02): k = 1 convs 4.55 vs 5.01 ms on
+// conv_gemm_kernel, the ConvTranspose phases 8.30 vs 7.44 ms (so they stay there)
+bool use_convp(const ConvArgs &a, int phases) {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("ACEHIP_CONVP");
-        v = (e && e[0] == '1') ? 1 : 0;
+        v = e ? (e[0] == '1' ? 1 : 0) : 2;
     }
-    return v == 1;
+    return v == 1 || (v == 2 && a.taps == 1 && phases == 1);
 }
 
 // ACEHIP_RU7=0 keeps the C = 128 residual units on conv7_kernel<FUSED> (A/B knob)
@@ -1325,7 +1327,7 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
     }
     const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
     if (tiles >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
-    if (use_convp() && a.taps * a.Cin / BK >= 3 && a.N <= cp::MAXN) {   // ≥ 3 K-tiles per item (vmcnt bookkeeping)
+    if (use_convp(a, phases) && a.taps * a.Cin / BK >= 3 && a.N <= cp::MAXN) {   // ≥ 3 K-tiles per item (vmcnt bookkeeping)
         const int64_t items = tiles * phases;
         const int nb = (int)std::min<int64_t>(items, num_cus_conv());
         const bool rs = a.res != nullptr, raw = a.out != nullptr, sn = a.out_s != nullptr;
