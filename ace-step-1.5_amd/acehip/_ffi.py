@@ -21,7 +21,7 @@ EXPORTS = [
     "acehip_get_version", "acehip_last_error",
     "acehip_dit_create", "acehip_dit_set_weight", "acehip_dit_finalize",
     "acehip_dit_set_condition", "acehip_dit_set_uniform_rows", "acehip_dit_forward", "acehip_dit_destroy",
-    "acehip_dit_set_graph",
+    "acehip_dit_set_graph", "acehip_dit_set_timesteps", "acehip_dit_forward_step",
     "acehip_dit_profile", "acehip_dit_profile_read", "acehip_dit_profile_kinds",
     "acehip_sampler_apg_euler", "acehip_sampler_adg_euler", "acehip_sampler_axpy",
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
@@ -72,6 +72,8 @@ def _declare(lib):
         "acehip_dit_forward": (c_int, [P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, P, P]),
         "acehip_dit_destroy": (c_int, [P]),
         "acehip_dit_set_graph": (c_int, [P, c_int]),
+        "acehip_dit_set_timesteps": (c_int, [P, P, P, c_int, P]),
+        "acehip_dit_forward_step": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
         "acehip_dit_profile": (c_int, [P, c_int]),
         "acehip_dit_profile_kinds": (c_int, [P, ctypes.c_uint]),
         "acehip_dit_profile_read": (c_int, [P, c_int, POINTER(c_int), POINTER(c_float)]),

@@ -19,6 +19,7 @@ fallback (``_ffi.lib()`` raises if the library is absent).
 from __future__ import annotations
 
 import inspect
+import os
 import math
 import time
 from typing import Dict, List, Optional, Union
@@ -135,6 +136,29 @@ class DiTRuntime:
         dt = ACEHIP_F32 if self.dtype == torch.float32 else ACEHIP_BF16
         check(lib().acehip_dit_forward(self.h, ptr(xt), ptr(ctx), Bx, ptr(t), ptr(t_r), stride, Bc, T, dt,
                                        ptr(out), stream_ptr()), "dit_forward")
+        return out
+
+    def set_timesteps(self, t: torch.Tensor, t_r: Optional[torch.Tensor] = None):
+        """Timestep MLPs of a whole schedule (one broadcast t per step, fp32 device tensor of
+        n steps); forward_step(i) then runs step i without re-reading the MLP weights."""
+        t = t.float().contiguous()
+        t_r = t if t_r is None else t_r.float().contiguous()
+        assert t.dim() == 1 and t_r.shape == t.shape
+        self._ts = (t, t_r)          # keep the arrays alive while the kernels read them
+        check(lib().acehip_dit_set_timesteps(self.h, ptr(t), ptr(t_r), t.numel(), stream_ptr()), "dit_set_timesteps")
+
+    def forward_step(self, xt: torch.Tensor, ctx: torch.Tensor, step: int,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """forward(xt, ctx, t[step]) of the set_timesteps schedule (bit-identical, bf16)."""
+        Bx, T, _ = xt.shape
+        Bc = self.Bc
+        assert Bc is not None, "set_condition first"
+        assert xt.dtype == self.dtype == ctx.dtype == torch.bfloat16
+        assert xt.is_contiguous() and ctx.is_contiguous() and ctx.shape[:2] == xt.shape[:2]
+        if out is None:
+            out = torch.empty(Bc, T, 64, device=xt.device, dtype=self.dtype)
+        check(lib().acehip_dit_forward_step(self.h, ptr(xt), ptr(ctx), Bx, int(step), Bc, T, ACEHIP_BF16,
+                                            ptr(out), stream_ptr()), "dit_forward_step")
         return out
 
     def use_graph(self, enable: bool = True):
@@ -359,6 +383,12 @@ class AceStepDiTBackend:
         costs["total_time_cost"] = t2 - t0
         return {"target_latents": xt, "time_costs": costs}
 
+    def _use_steps(self) -> bool:
+        """Schedule-wide timestep MLPs (acehip_dit_set_timesteps) for the bf16 runtime;
+        ACEHIP_DIT_STEPS=0 runs every step through acehip_dit_forward (A/B)."""
+        return (self.dtype == torch.bfloat16 and hasattr(self.rt, "set_timesteps")
+                and os.environ.get("ACEHIP_DIT_STEPS", "1") != "0")
+
     def _set_cond(self, enc, cfg):
         if cfg:
             B = enc.shape[0]
@@ -404,12 +434,15 @@ class AceStepDiTBackend:
         ra = torch.zeros_like(xt) if do_cfg else None
         first = True
         switched = False
+        steps_api = self._use_steps()
+        if steps_api:
+            self.rt.set_timesteps(t_dev[:n])
         for i in range(n):
             if i >= cover_steps and not switched:
                 switched = True
                 self._set_cond(enc_nc.to(device, dtype), do_cfg)
                 ctx = ctx_nc.to(device=device, dtype=dtype).contiguous()
-            vt = self.rt.forward(xt, ctx, t_dev[i:i + 1])
+            vt = self.rt.forward_step(xt, ctx, i) if steps_api else self.rt.forward(xt, ctx, t_dev[i:i + 1])
             apply = (1 if cfg_on[i] else 0) if do_cfg else -1
             adg = use_adg and apply == 1          # ADG replaces APG inside the CFG interval (base:1949-1964)
             if method == "sde":
@@ -452,12 +485,15 @@ class AceStepDiTBackend:
         method = kw.get("infer_method", "ode")
         self._set_cond(enc, False)
         switched = False
+        steps_api = self._use_steps()
+        if steps_api:
+            self.rt.set_timesteps(t_dev[:n])
         for i in range(n):
             if i >= cover_steps and not switched:
                 switched = True
                 self._set_cond(enc_nc.to(device, dtype), False)
                 ctx = ctx_nc.to(device=device, dtype=dtype).contiguous()
-            vt = self.rt.forward(xt, ctx, t_dev[i:i + 1])
+            vt = self.rt.forward_step(xt, ctx, i) if steps_api else self.rt.forward(xt, ctx, t_dev[i:i + 1])
             if i == n - 1:
                 axpy_(vt, xt, tv[i])                               # x0 = xt − vt·t (turbo:1975-1977)
                 break

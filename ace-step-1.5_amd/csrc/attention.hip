@@ -473,10 +473,20 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
         __syncthreads();
         if (s_ticket != nsplit - 1) return;
+        // merge ALL parts (this one re-read too) in part order: the result does not depend on
+        // which part finished last (bit-reproducible from run to run)
         for (int p2 = 0; p2 < nsplit; ++p2) {
-            if (p2 == part) continue;
             const float *oth = sp.ws + (((int64_t)(u - sp.full) * nsplit + p2) * 8 + wave) * wsz;
             const float m2 = ld_c(oth + 64 * 64 + lane), l2 = ld_c(oth + 65 * 64 + lane);
+            if (p2 == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) oacc[i][j] = ld_c(oth + (16 * i + j) * 64 + lane);
+                l = l2;
+                m = m2;
+                continue;
+            }
             const float mn = fmaxf(m, m2);
             const float a1 = __builtin_amdgcn_exp2f(m - mn), a2 = __builtin_amdgcn_exp2f(m2 - mn);
 #pragma unroll
@@ -1005,12 +1015,20 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
         __syncthreads();
         if (s_ticket != nsplit - 1) return;
-        for (int p2 = 0; p2 < nsplit; ++p2) {
-            if (p2 == part) continue;
+        for (int p2 = 0; p2 < nsplit; ++p2) {          // all parts in part order (reproducible)
 #pragma unroll
             for (int sb = 0; sb < 2; ++sb) {
                 const float *oth = sp.ws + (((int64_t)(u - sp.full) * nsplit + p2) * 8 + 2 * wave + sb) * wsz;
                 const float m2 = ld_c(oth + 64 * 64 + lane), l2 = ld_c(oth + 65 * 64 + lane);
+                if (p2 == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) oacc[sb][i][j] = ld_c(oth + (16 * i + j) * 64 + lane);
+                    l[sb] = l2;
+                    m[sb] = m2;
+                    continue;
+                }
                 const float mm = fmaxf(m[sb], m2);
                 const float a1 = __builtin_amdgcn_exp2f(m[sb] - mm), a2 = __builtin_amdgcn_exp2f(m2 - mm);
 #pragma unroll

@@ -74,6 +74,10 @@ struct acehip_dit {
     // constant V row and their cross-O output the per-layer constant cnull[l]
     int uniform_from = 1 << 30;
     bf16_t *cnull = nullptr, *vnull = nullptr;   // [L][D], [q_dim]
+    // timestep MLP outputs of a whole schedule (acehip_dit_set_timesteps): row i = step i's
+    // temb [D] and proj [6D]; ts_scratch holds the batched MLP intermediates
+    int ts_n = 0, ts_cap = 0;
+    bf16_t *ts_temb = nullptr, *ts_proj = nullptr, *ts_scratch = nullptr;
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
     void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs (short songs / turbo)
     size_t tmp_elems = 0;
@@ -111,8 +115,12 @@ struct acehip_dit {
     } f{};
 };
 
-static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s);
+static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, hipStream_t s);
+static int timestep_mlps(acehip_dit *h, const bf16_t *const emb[2], int rows, bf16_t *h1, bf16_t *const temb_e[2],
+                         bf16_t *const proj_e[2], bf16_t *temb, bf16_t *proj, hipStream_t s);
 static int knob_hash();
+static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, const float *t, const float *t_r,
+                        int t_stride, int step, int Bc, int T, void *vt_out, hipStream_t s);
 static int create_f32(acehip_dit *h);
 static int set_weight_f32(acehip_dit *h, Slot &s, const void *ptr, int dtype, int64_t n, int on_device);
 static int build_rope_f32(acehip_dit *h);
@@ -542,52 +550,63 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx, c
     hipStream_t s = (hipStream_t)stream;
     if (h->f32)
         return forward_f32(h, (const float *)xt, (const float *)ctx, Bx, t, t_r, t_stride, Bc, T, (float *)vt_out, s);
-    const int M = Bc * S;
-    int rc;
-#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
-    // the only reads of t / xt / ctx: sinusoid embeddings and patch packing (base:1340-1358)
-    for (int e = 0; e < 2; ++e) RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
-    RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
-    // CFG: every batch row reads xt/ctx row 0 (Bx = 1) at one broadcast t, so the rows are
-    // identical until the first cross-attention — proj_in and layer 0's self-attention
-    // block run on row 0 only and are copied (ACEHIP_DIT_DEDUP=0 disables, for A/B)
-    const char *de = getenv("ACEHIP_DIT_DEDUP");
-    const bool dup = Bx == 1 && Bc > 1 && t_stride == 0 && !(de && de[0] == '0');
-    if (!h->graph_on || h->prof) {
-        RUN(forward_body(h, Bc, S, dup, s));
-    } else {
-        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), dup ? 1 : 0, knob_hash()};
-        if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
-            if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
-            if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
-            HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
-            const int brc = forward_body(h, Bc, S, dup, h->cap_stream);
-            hipGraph_t g = nullptr;
-            const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
-            if (brc) { if (g) (void)hipGraphDestroy(g); return brc; }
-            if (ec != hipSuccess || !g) return fail(ACEHIP_E_HIP, "forward: graph capture failed");
-            const hipError_t ei = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            if (ei != hipSuccess) { h->gexec = nullptr; return fail(ACEHIP_E_HIP, "forward: graph instantiate failed"); }
-            memcpy(h->gkey, key, sizeof(key));
-        }
-        HIP_TRY(hipGraphLaunch(h->gexec, s));
-    }
-    // proj_out (base:1491-1501) on the normed output XN
-    GemmArgs po{};
-    po.A = h->XN; po.lda = h->D; po.W = h->wout; po.ldw = h->D;
-    po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
-    po.M = M; po.N = 128; po.K = h->D; po.epi = EPI_STORE; po.bias = h->bout;
-    RUN(hgemm(h, po, s));
-    if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
-#undef RUN
-    return 0;
+    return forward_bf16(h, xt, ctx, Bx, t, t_r, t_stride, -1, Bc, T, vt_out, s);
 }
 
 int acehip_dit_set_graph(acehip_dit *h, int enable) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
     h->graph_on = enable != 0 && !h->f32;
     return 0;
+}
+
+int acehip_dit_set_timesteps(acehip_dit *h, const float *t, const float *t_r, int n_steps, void *stream) {
+    if (!h || !t || !t_r) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized) return fail(ACEHIP_E_STATE, "set_timesteps before finalize");
+    if (h->f32) return fail(ACEHIP_E_STATE, "set_timesteps: bf16 handles only (the fp32 parity mode runs per step)");
+    if (n_steps <= 0 || n_steps > 4096) return fail(ACEHIP_E_ARG, "set_timesteps: n_steps in [1, 4096]");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int D = h->D;
+    if (n_steps > h->ts_cap) {
+        HIP_TRY(hipStreamSynchronize(s));
+        for (bf16_t *p : {h->ts_temb, h->ts_proj, h->ts_scratch})
+            if (p) (void)hipFree(p);
+        h->ts_temb = h->ts_proj = h->ts_scratch = nullptr;
+        h->ts_cap = h->ts_n = 0;
+        const int cap = std::max(n_steps, 64);
+        // scratch: emb [2][cap][256], h1 [cap][D], temb_e [2][cap][D], proj_e [2][cap][6D]
+        const size_t scratch = (size_t)cap * (2 * 256 + D + 2 * D + 2 * 6 * D);
+        HIP_TRY(hipMalloc(&h->ts_temb, (size_t)cap * D * 2));
+        HIP_TRY(hipMalloc(&h->ts_proj, (size_t)cap * 6 * D * 2));
+        HIP_TRY(hipMalloc(&h->ts_scratch, scratch * 2));
+        h->ts_cap = cap;
+    }
+    const size_t cap = h->ts_cap;
+    bf16_t *emb[2] = {h->ts_scratch, h->ts_scratch + cap * 256};
+    bf16_t *h1 = h->ts_scratch + cap * 512;
+    bf16_t *temb_e[2] = {h1 + cap * D, h1 + cap * 2 * D};
+    bf16_t *proj_e[2] = {h1 + cap * 3 * D, h1 + cap * 9 * D};
+    int rc;
+    // one sinusoid row per step (t[i], t_r[i]), then the MLPs over all steps: the MLP weights
+    // are read once per schedule instead of once per step
+    for (int e = 0; e < 2; ++e)
+        if ((rc = timestep_sinusoid(t, t_r, 1, e, n_steps, h->freqs, emb[e], s))) return rc;
+    if ((rc = timestep_mlps(h, emb, n_steps, h1, temb_e, proj_e, h->ts_temb, h->ts_proj, s))) return rc;
+    h->ts_n = n_steps;
+    return 0;
+}
+
+int acehip_dit_forward_step(acehip_dit *h, const void *xt, const void *ctx, int Bx, int step, int Bc, int T,
+                            int dtype, void *vt_out, void *stream) {
+    if (!h || !xt || !ctx || !vt_out) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized || !h->have_cond) return fail(ACEHIP_E_STATE, "forward_step before finalize/set_condition");
+    if (h->f32 || dtype != ACEHIP_BF16) return fail(ACEHIP_E_ARG, "forward_step: bf16 handles only");
+    if (step < 0 || step >= h->ts_n) return fail(ACEHIP_E_STATE, "forward_step: step outside the set_timesteps schedule");
+    if (Bc != h->cond_Bc) return fail(ACEHIP_E_ARG, "forward_step: Bc differs from set_condition");
+    const int S = (T + 1) / 2;
+    if (T <= 0 || S > h->cfg.max_S || Bx <= 0 || Bc % Bx) return fail(ACEHIP_E_ARG, "forward_step: T/Bx out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    return forward_bf16(h, xt, ctx, Bx, nullptr, nullptr, 0, step, Bc, T, vt_out, (hipStream_t)stream);
 }
 
 }  // extern "C"
@@ -610,20 +629,94 @@ static int knob_hash() {
 
 // Everything of one forward between the input packing and proj_out: reads only handle
 // buffers (emb, Xin, weights, K/V cache), so it can be captured once and replayed.
-static int forward_body(acehip_dit *h, int Bc, int S, bool dup, hipStream_t s) {
+// bf16 forward; step >= 0 takes the timestep MLP outputs from the set_timesteps cache
+static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, const float *t, const float *t_r,
+                        int t_stride, int step, int Bc, int T, void *vt_out, hipStream_t s) {
+    const int S = (T + 1) / 2;
+    const int M = Bc * S;
+    int rc;
+#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
+    // the only reads of t / xt / ctx: sinusoid embeddings and patch packing (base:1340-1358);
+    // step >= 0: the schedule's precomputed timestep MLP row (acehip_dit_set_timesteps)
+    const bool ts_cached = step >= 0;
+    if (ts_cached) {
+        RUN(bcast_rows(h->ts_temb + (size_t)step * h->D, h->D, h->temb, Bc, s));
+        RUN(bcast_rows(h->ts_proj + (size_t)step * 6 * h->D, 6 * h->D, h->proj, Bc, s));
+    } else {
+        for (int e = 0; e < 2; ++e) RUN(timestep_sinusoid(t, t_r, t_stride, e, Bc, h->freqs, h->emb[e], s));
+    }
+    RUN(pack_patches((const bf16_t *)xt, (const bf16_t *)ctx, Bx, Bc, T, S, h->Xin, s));
+    // CFG: every batch row reads xt/ctx row 0 (Bx = 1) at one broadcast t, so the rows are
+    // identical until the first cross-attention — proj_in and layer 0's self-attention
+    // block run on row 0 only and are copied (ACEHIP_DIT_DEDUP=0 disables, for A/B)
+    const char *de = getenv("ACEHIP_DIT_DEDUP");
+    const bool dup = Bx == 1 && Bc > 1 && (ts_cached || t_stride == 0) && !(de && de[0] == '0');
+    if (!h->graph_on || h->prof) {
+        RUN(forward_body(h, Bc, S, dup, ts_cached, s));
+    } else {
+        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), (dup ? 1 : 0) | (ts_cached ? 2 : 0),
+                            knob_hash()};
+        if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
+            if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
+            if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+            HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
+            const int brc = forward_body(h, Bc, S, dup, ts_cached, h->cap_stream);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(h->cap_stream, &g);
+            if (brc) { if (g) (void)hipGraphDestroy(g); return brc; }
+            if (ec != hipSuccess || !g) return fail(ACEHIP_E_HIP, "forward: graph capture failed");
+            const hipError_t ei = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ei != hipSuccess) { h->gexec = nullptr; return fail(ACEHIP_E_HIP, "forward: graph instantiate failed"); }
+            memcpy(h->gkey, key, sizeof(key));
+        }
+        HIP_TRY(hipGraphLaunch(h->gexec, s));
+    }
+    // proj_out (base:1491-1501) on the normed output XN
+    GemmArgs po{};
+    po.A = h->XN; po.lda = h->D; po.W = h->wout; po.ldw = h->D;
+    po.C = (T % 2 == 0) ? (bf16_t *)vt_out : h->O2; po.ldc = 128;
+    po.M = M; po.N = 128; po.K = h->D; po.epi = EPI_STORE; po.bias = h->bout;
+    RUN(hgemm(h, po, s));
+    if (T % 2) RUN(crop_rows(h->O2, Bc, 2 * S, T, 64, (bf16_t *)vt_out, s));
+#undef RUN
+    return 0;
+}
+
+
+#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
+// timestep embeddings: temb = temb_t + temb_r, proj = proj_t + proj_r (base:1340-1344) for
+// `rows` rows of sinusoid embeddings, in chunks of 16 rows (gemv_small computes every row
+// with the same instruction sequence whatever the row count, so a row's result does not
+// depend on how many rows share the launch)
+static int timestep_mlps(acehip_dit *h, const bf16_t *const emb[2], int rows, bf16_t *h1, bf16_t *const temb_e[2],
+                         bf16_t *const proj_e[2], bf16_t *temb, bf16_t *proj, hipStream_t s) {
+    const int D = h->D;
+    int rc;
+    for (int r0 = 0; r0 < rows; r0 += 16) {
+        const int n = std::min(16, rows - r0);
+        for (int e = 0; e < 2; ++e) {
+            RUN(gemv_small(emb[e] + (size_t)r0 * 256, 256, h->te_l1[e], h->te_b1[e], h1 + (size_t)r0 * D, D, n, D,
+                           256, 0, s));
+            RUN(gemv_small(h1 + (size_t)r0 * D, D, h->te_l2[e], h->te_b2[e], temb_e[e] + (size_t)r0 * D, D, n, D, D,
+                           1, s));
+            RUN(gemv_small(temb_e[e] + (size_t)r0 * D, D, h->te_tp[e], h->te_btp[e], proj_e[e] + (size_t)r0 * 6 * D,
+                           6 * D, n, 6 * D, D, 1, s));
+        }
+    }
+    RUN(add_bf16(temb_e[0], temb_e[1], temb, (int64_t)rows * D, s));
+    RUN(add_bf16(proj_e[0], proj_e[1], proj, (int64_t)rows * 6 * D, s));
+    return 0;
+}
+
+static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, hipStream_t s) {
     const int D = h->D, F = h->F, qd = h->qd, kvd = h->kvd, L = h->L, M = Bc * S;
     const int H = h->cfg.heads, KV = h->cfg.kv_heads, Le = h->cond_Lenc;
     const float eps = h->cfg.eps, scale = 1.0f / sqrtf((float)h->cfg.head_dim);
     int rc;
-#define RUN(x) do { if ((rc = (x))) return rc; } while (0)
-    // timestep embeddings: temb = temb_t + temb_r, proj = proj_t + proj_r (base:1340-1344)
-    for (int e = 0; e < 2; ++e) {
-        RUN(gemv_small(h->emb[e], 256, h->te_l1[e], h->te_b1[e], h->h1, D, Bc, D, 256, 0, s));
-        RUN(gemv_small(h->h1, D, h->te_l2[e], h->te_b2[e], h->temb_e[e], D, Bc, D, D, 1, s));
-        RUN(gemv_small(h->temb_e[e], D, h->te_tp[e], h->te_btp[e], h->proj_e[e], 6 * D, Bc, 6 * D, D, 1, s));
-    }
-    RUN(add_bf16(h->temb_e[0], h->temb_e[1], h->temb, (int64_t)Bc * D, s));
-    RUN(add_bf16(h->proj_e[0], h->proj_e[1], h->proj, (int64_t)Bc * 6 * D, s));
+    // timestep MLPs (temb, proj), unless acehip_dit_forward_step already broadcast the
+    // schedule's precomputed row into h->temb / h->proj
+    if (!ts_cached) RUN(timestep_mlps(h, h->emb, Bc, h->h1, h->temb_e, h->proj_e, h->temb, h->proj, s));
     RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s));
     RUN(modulation(h->sst_out, 1, 2, h->temb, Bc, D, h->mod_out, s));
 
@@ -750,6 +843,8 @@ int acehip_dit_destroy(acehip_dit *h) {
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     for (void *p : h->allocs) (void)hipFree(p);
+    for (bf16_t *p : {h->ts_temb, h->ts_proj, h->ts_scratch})
+        if (p) (void)hipFree(p);
     delete h;
     return 0;
 }

@@ -51,6 +51,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / t
 int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
                int64_t ldy, int M, int N, int K, int act, hipStream_t s);
 // sinusoid of bf16(t*1000): emb[b][0:128]=cos, [128:256]=sin, as bf16 (base:225-246)
+// dst[r][0..n) = src[0..n) for r < rows (n % 8 == 0)
+int bcast_rows(const bf16_t *src, int64_t n, bf16_t *dst, int rows, hipStream_t s);
 int timestep_sinusoid(const float *t, const float *t_r, int t_stride, int use_diff, int Bc,
                       const float *freqs, bf16_t *emb, hipStream_t s);
 // out = bf16(a + b) elementwise

@@ -48,6 +48,13 @@ __global__ __launch_bounds__(256) void gemv_small_kernel(const bf16_t *__restric
     }
 }
 
+// dst row r (r = blockIdx.y) = src, 16 B per lane
+__global__ __launch_bounds__(256) void bcast_rows_kernel(const bf16_t *__restrict__ src, int64_t n,
+                                                         bf16_t *__restrict__ dst) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (i < n) *(uint4 *)(dst + blockIdx.y * n + i) = *(const uint4 *)(src + i);
+}
+
 __global__ void sinusoid_kernel(const float *t, const float *t_r, int t_stride, int use_diff,
                                 const float *freqs, bf16_t *emb) {
     const int b = blockIdx.x, i = threadIdx.x;  // 128 threads
@@ -270,6 +277,13 @@ int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias
                int64_t ldy, int M, int N, int K, int act, hipStream_t s) {
     if (M > 16 || K % 8 || ldx % 8) return fail(-1, "gemv_small: M<=16, K%8==0 required");
     gemv_small_kernel<<<(N + 3) / 4, 256, 0, s>>>(x, ldx, W, bias, y, ldy, M, N, K, act);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int bcast_rows(const bf16_t *src, int64_t n, bf16_t *dst, int rows, hipStream_t s) {
+    if (n % 8) return fail(-1, "bcast_rows: n % 8");
+    bcast_rows_kernel<<<dim3((unsigned)((n / 8 + 255) / 256), rows), 256, 0, s>>>(src, n, dst);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -118,6 +118,17 @@ int acehip_dit_forward(acehip_dit *h, const void *xt, const void *ctx, int Bx,
                        const float *t, const float *t_r, int t_stride, int Bc, int T,
                        int dtype, void *vt_out, void *stream);
 
+/* Timestep MLPs of a whole schedule at once: t, t_r are device fp32 arrays of n_steps
+ * entries, one broadcast timestep pair per step (the t-dependent part of
+ * AceStepDiTModel.forward, base:1340-1344, evaluated for every step of the sampler loop
+ * base:1936 / turbo:1968 up front).  acehip_dit_forward_step(step) is then
+ * acehip_dit_forward with t = t[step], t_r = t_r[step], t_stride 0, except that the ~108 MB
+ * of timestep-MLP weights are read once per schedule instead of once per step — bit-
+ * identical (each MLP row is computed by the same instruction sequence).  bf16 handles. */
+int acehip_dit_set_timesteps(acehip_dit *h, const float *t, const float *t_r, int n_steps, void *stream);
+int acehip_dit_forward_step(acehip_dit *h, const void *xt, const void *ctx, int Bx, int step, int Bc, int T,
+                            int dtype, void *vt_out, void *stream);
+
 /* Replay the pointer-independent middle of acehip_dit_forward (timestep MLPs,
  * modulation, proj_in, the layer stack, norm_out) as one HIP graph, captured
  * once per (Bc, S, Lenc, uniform rows) and re-captured when they change or

@@ -88,13 +88,17 @@ def test_attention_tail_split(gpu_device, monkeypatch, cus, window, pw):
     q = torch.randn(B, H, Sq, 128, generator=g).to(gpu_device, torch.bfloat16)
     k = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
     v = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
-    for _ in range(2):                          # second launch checks the counters self-reset
+    outs = []
+    for _ in range(3):                          # later launches check the counters self-reset
         o = torch.empty(B, Sq, H * 128, device=gpu_device, dtype=torch.bfloat16)
         ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, Sq, Sk,
                                                 window, 1 / math.sqrt(128), ff.stream_ptr()))
         torch.cuda.synchronize()
         ref = _attn_ref(q, k, v, window).transpose(1, 2).reshape(B, Sq, H * 128)
         assert rel_l2(o.float().cpu(), ref.float().cpu()) < 1e-2
+        outs.append(o)
+    # the parts are merged in part order whichever finishes last: bit-reproducible
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 def _attn_ref(q, k, v, window):
@@ -318,11 +322,19 @@ def test_generate_audio_per_step_parity(gpu_device):
     seen = []
     orig = rt.forward
 
+    orig_step = rt.forward_step
+
     def spy(xt, c, t, t_r=None, out=None):
         vt = orig(xt, c, t, t_r, out)
         seen.append((xt.clone(), t.clone(), vt.clone()))
         return vt
+
+    def spy_step(xt, c, step, out=None):      # the production path (acehip_dit_forward_step)
+        vt = orig_step(xt, c, step, out)
+        seen.append((xt.clone(), rt._ts[0][step:step + 1].clone(), vt.clone()))
+        return vt
     rt.forward = spy
+    rt.forward_step = spy_step
     res = be.generate_audio(encoder_hidden_states=enc.to(gpu_device), context_latents=ctx.to(gpu_device),
                             infer_steps=4, diffusion_guidance_sale=7.0, shift=3.0, seed=[0, 1])
     torch.cuda.synchronize()
@@ -602,4 +614,33 @@ def test_null_row_add_fused_into_norm(gpu_device, monkeypatch):
     fused = rt.forward(xt, ctx, t)
     torch.cuda.synchronize()
     assert torch.equal(sep, fused)
+    rt.close()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_forward_step_matches_forward(gpu_device, graph):
+    """acehip_dit_set_timesteps + forward_step(i) (timestep MLPs of the whole schedule in one
+    pass, 40 steps = 3 row chunks) is bit-identical to forward(t[i]) for every step, with and
+    without the HIP graph; t_r != t exercises the second (t − t_r) embedding."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=2, window=16)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=9, mode="parity").items()}
+    g = torch.Generator().manual_seed(41)
+    rt = DiTRuntime(cfg, 0, max_S=128, max_Bc=2, max_Lenc=64)
+    rt.load(W)
+    rt.use_graph(graph)
+    xt = torch.randn(1, 201, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(1, 201, 128, generator=g).bfloat16().to(gpu_device)
+    rt.set_condition(torch.randn(2, 30, cfg.hidden_size, generator=g).bfloat16().to(gpu_device))
+    n = 40
+    t = torch.linspace(1.0, 0.05, n, device=gpu_device, dtype=torch.float32)
+    t_r = (t * 0.5).contiguous()
+    rt.set_timesteps(t, t_r)
+    for i in [0, 1, 15, 16, 17, 39]:
+        a = rt.forward(xt, ctx, t[i:i + 1], t_r[i:i + 1]).clone()
+        b = rt.forward_step(xt, ctx, i)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), i
+    with pytest.raises(RuntimeError):
+        rt.forward_step(xt, ctx, n)                  # outside the schedule
     rt.close()
