@@ -667,6 +667,17 @@ __device__ __forceinline__ void pw_kread(uint32_t lane_off) {
 }
 // XDL (8 passes) → VALU read of its result: 12 wait states
 __device__ __forceinline__ void xdl_pad(f32x16 &a, f32x16 &b) { asm volatile("s_nop 7\n\ts_nop 4" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ const void *pw_uniform(const void *p) {   // pointer known wave-uniform → SGPRs
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void *)(((uint64_t)hi << 32) | lo);
+}
+// LDS-DMA of one 1 KiB piece, saddr form (SGPR base, per-lane 32-bit offset); M0 (the LDS
+// destination) is written in the same statement
+__device__ __forceinline__ void pw_dma(const char *base, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr), "v"(voff),
+                 "s"(base) : "memory");
+}
 template <int A>
 __device__ __forceinline__ void pw_qload(const bf16_t *p) {
     asm volatile("global_load_dwordx4 a[%c0:%c1], %2, off" :: "n"(A), "n"(A + 3), "v"(p) : "memory");
@@ -756,7 +767,28 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         ntiles = t1 - t0;
     }
     // 32 KiB tile = 32 LDS-DMA wave-instructions, 8 per wave
+    // Whole tiles (kv0 + 64 ≤ Sk) go by the saddr form: SGPR base = K or V + the piece's first
+    // key row (uniform: waves 0-1 stage K, 2-3 V), VGPR = the lane's swizzled 16-B slot, one of
+    // four per-lane offsets (the swizzle of row 4(c & 3) + lane / 16) — no per-piece address
+    // VALU.  The last, partial tile clamps rows past Sk to a real row (per-lane addresses).
+    uint32_t dma_off[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = 4 * j + (lane >> 4);
+        dma_off[j] = (uint32_t)((lane >> 4) * 256 + (((lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4));
+    }
+    const char *kv_src = (const char *)pw_uniform(wave < 2 ? kp : vp);
+    const uint32_t lds_u = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
     auto stage_tile = [&](int kv0, int buf) __attribute__((always_inline)) {
+        if (kv0 + KT <= Sk) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int c = wave * 8 + i;
+                pw_dma(kv_src + (int64_t)(kv0 + (c & 15) * 4) * 256, dma_off[i & 3],
+                       lds_u + ((c >> 4) * NBUF + buf) * TILE + (c & 15) * 1024);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int c = wave * 8 + i;
