@@ -300,20 +300,24 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a, int sp
 // + 2·NW·it, so (batch, position) advance incrementally (no integer division per unit)
 // and every cos/sin row is loaded BEFORE the first store (a load's vmcnt would
 // otherwise also wait for the older stores).
-template <int BM, int NW, int LDS_BYTES, typename StoreAcc>
+//
+// HPT = 1: a BM×128 tile holds one head; the four 16-lane groups of a wave take four rows.
+template <int BM, int NW, int LDS_BYTES, int HPT, typename StoreAcc>
 __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, int m0, int n0, int wave, int lane,
                                                   StoreAcc store_acc) {
-    constexpr int PITCH = 264;   // 528-B rows: 16-B aligned, 2-way conflicts on the 8-B writes
-    constexpr int RPI = 2 * NW;  // rows per iteration
+    static_assert(HPT == 1 || HPT == 2, "one or two heads per tile");
+    constexpr int PITCH = 128 * HPT + 8;   // 16-B aligned rows, 2-way conflicts on the 8-B writes
+    constexpr int RPW = 4 / HPT;           // rows per wave per iteration
+    constexpr int RPI = RPW * NW;          // rows per iteration
     constexpr int ITER = BM / RPI;
     static_assert(BM % RPI == 0, "rows must split evenly over the iterations");
     static_assert(BM * PITCH * 2 <= LDS_BYTES, "head-post staging tile must fit the operand ring");
     const HeadPostArgs &h = a.hp;
-    const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = sub & 1;
+    const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = HPT == 2 ? sub & 1 : 0;
     const int head = (n0 >> 7) + hh;
     const bool norm = head < h.nq + h.nk;
     const bool rope = h.cos != nullptr;
-    const int r0 = wave * 2 + (sub >> 1);
+    const int r0 = wave * RPW + (HPT == 2 ? sub >> 1 : sub);
     const int mf = min(m0 + r0, a.M - 1);
     const int b0 = mf / h.S, s0 = mf - b0 * h.S;
     uint4 cv[ITER], sv[ITER];
@@ -607,7 +611,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     if (wr == 0) bar();   // balance the barrier count
 
     if constexpr (EPI == EPI_HEADPOST) {
-        headpost_epilogue<BM, 8, sizeof(lds)>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
+        headpost_epilogue<BM, 8, sizeof(lds), 2>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
             for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -757,8 +761,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     // before their accumulators are read
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     if constexpr (EPI == EPI_HEADPOST) {
-        static_assert(BN == 256, "head-post tiles hold two 128-column heads");
-        headpost_epilogue<BM, 4, sizeof(lds)>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
+        headpost_epilogue<BM, 4, sizeof(lds), BN / 128>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
             for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -782,7 +785,7 @@ int launch_w4(const GemmArgs &a, hipStream_t s) {
         case EPI_RES: gemm_w4_kernel<BM, BN, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
         case EPI_SWIGLU: gemm_w4_kernel<BM, BN, EPI_SWIGLU><<<tiles, 256, 0, s>>>(a); break;
         case EPI_HEADPOST:
-            if constexpr (BM == 192 && BN == 256) {
+            if constexpr (BM == 192 && (BN == 256 || BN == 128)) {
                 gemm_w4_kernel<BM, BN, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
                 break;
             }
@@ -1016,12 +1019,15 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         }
     }
     if (a.epi == EPI_HEADPOST) {
-        // the fused epilogue exists for the 192-row tile only; a grid of it that fills at
-        // most half the chip (cross-Q of the conditional rows, M = 3000) runs as 128×128
-        // tiles into the staging buffer + the standalone head_post kernel instead
+        // a 192×256 grid that fills at most half the chip (cross-Q of the conditional rows,
+        // M = 3000) runs as 192×128 tiles — one head each — with the same fused epilogue;
+        // ACEHIP_GEMM_HP128=2: those tiles into the staging buffer + the standalone
+        // head_post kernel (the previous path), =0: the 192×256 grid regardless
         const int64_t t192 = (int64_t)((a.M + 191) / 192) * (a.N / 256);
         const char *e = getenv("ACEHIP_GEMM_HP128");
-        if (a.ws && t192 * 2 <= num_cus() && (size_t)a.M * a.N * 2 <= a.ws_bytes && !(e && e[0] == '0')) {
+        const bool small = t192 * 2 <= num_cus() && !(e && e[0] == '0');
+        if (small && use_w4s(a.M, a.N) && !(e && e[0] == '2')) return launch_w4<192, 128>(a, s);
+        if (small && a.ws && (size_t)a.M * a.N * 2 <= a.ws_bytes) {
             GemmArgs st = a;
             st.epi = EPI_STORE;
             st.bias = nullptr;

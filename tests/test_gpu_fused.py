@@ -45,6 +45,8 @@ def _headpost_ref(C, B, S, nq, nk, nv, qw, kw, cos, sin, eps):
     (2, 250, 4, 0, 0, 192, False),     # cross-attention Q: q heads only, no RoPE
     (3, 65, 2, 2, 4, 64, True),        # one K-tile, B·S not a multiple of S-tiles
     (1, 125, 16, 8, 8, 2048, True),    # short song: split-K partials + standalone head_post
+    (1, 3000, 16, 0, 0, 2048, False),  # cross-Q of the cond rows: half-chip grid → 192×128 one-head tiles
+    (1, 2990, 8, 4, 4, 256, True),     # same tile choice with k / v heads, RoPE and a ragged last tile
 ])
 def test_gemm_headpost_vs_oracle(gpu_device, B, S, nq, nk, nv, K, rope):
     ff = _ff()
