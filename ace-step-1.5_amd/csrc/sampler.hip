@@ -8,11 +8,13 @@
 //   vt = bf16(cond + bf16((g−1)·bf16(orth)));  xt = bf16(xt − bf16(vt·dt))
 // Storage type S = bf16 (production: every op output rounded to bf16 as torch
 // does) or float (the fp32 parity mode: the same chain with no rounding).
-// The norms are global per-(song, channel) reductions over T, so one
-// thread workgroup (512 threads) owns 8 channels of one song (16-B row accesses) and runs
-// three L2-resident passes with LDS reductions in between: no host sync, no
-// extra launches, 8 workgroups per song.  2.3 MB per song at 240 s.
+// The norms are global per-(song, channel) reductions over T: three launches
+// (see apg_phase_kernel), L2-resident passes, no host sync.  2.3 MB per song
+// at 240 s.  The chunk-partial workspace is one per device: calls on
+// different streams of one device must not overlap.
 #include "kernels.h"
+
+#include <map>
 
 namespace acehip {
 namespace {
@@ -36,117 +38,152 @@ __device__ __forceinline__ float ld1(const float *p) { return *p; }
 __device__ __forceinline__ void st1(bf16_t *p, float v) { *p = f2bf(v); }
 __device__ __forceinline__ void st1(float *p, float v) { *p = v; }
 
-// grid (8 channel groups, B songs); 512 threads = 512 rows in flight, each
-// thread owns 8 consecutive channels (one 16-B access per row)
-template <class S>
-__global__ __launch_bounds__(512) void apg_euler_kernel(const S *__restrict__ vt,
-                                                         S *__restrict__ xt,
-                                                         S *__restrict__ ra, int B, int T,
-                                                         float guidance, float dt, int apply_cfg,
-                                                         int first_step, int out_mode) {
-    constexpr int C = 64, CG = 8, NTH = 512, NW = NTH / 64;
+// The norms are reductions over all T rows of a (song, channel), so the step
+// runs as three launches over grid (8 channel groups, ⌈T/256⌉ row chunks, B
+// songs), one row per thread (8 channels = one 16-B access), with per-chunk
+// partial sums in a small workspace combined in chunk order (deterministic):
+//   phase 1  ra update (written), Σ ra² (fp32) and Σ cond² (fp64) per chunk
+//   phase 2  sf, ‖cond‖ from the phase-1 partials; Σ v0·v1 (fp64) per chunk
+//   phase 3  dot from the phase-2 partials; vt and the Euler update
+// (one workgroup per channel group walking all T rows was 78 µs per step at
+// T = 6000 on 8 CUs; the three launches spread it over 192 workgroups)
+constexpr int APG_TC = 256;
+struct ApgPart {
+    float ss[8];
+    double cs[8];
+    double dot[8];
+};
+
+// chunk partials of one (song, channel group) summed in chunk order, then over
+// the block: thread j < 8 owns channel j; results broadcast through LDS
+template <int PHASE>
+__device__ __forceinline__ void apg_totals(const ApgPart *p, int nch, float *sf, double *denom, double *dot) {
+    __shared__ float s_sf[8];
+    __shared__ double s_den[8], s_dot[8];
+    const int j = threadIdx.x;
+    if (j < 8) {
+        float a = 0.f;
+        double c = 0.0, d = 0.0;
+        for (int ch = 0; ch < nch; ++ch) {
+            a += p[ch].ss[j];
+            c += p[ch].cs[j];
+            if (PHASE == 3) d += p[ch].dot[j];
+        }
+        s_sf[j] = a;
+        s_den[j] = c;
+        s_dot[j] = d;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        sf[k] = s_sf[k];
+        denom[k] = s_den[k];
+        dot[k] = s_dot[k];
+    }
+}
+
+template <class S, int PHASE>
+__global__ __launch_bounds__(APG_TC) void apg_phase_kernel(const S *__restrict__ vt, S *__restrict__ xt,
+                                                         S *__restrict__ ra, int B, int T, float guidance,
+                                                         float dt, int first_step, int out_mode,
+                                                         ApgPart *__restrict__ part) {
+    constexpr int C = 64, CG = 8, NW = APG_TC / 64;
     __shared__ float s_ss[NW][CG];
     __shared__ double s_cs[NW][CG];
-    const int cg = blockIdx.x, b = blockIdx.y;
+    const int cg = blockIdx.x, ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t base = (int64_t)b * T * C + cg * CG;
-    const S *cond = vt + base;
-    const S *unc = vt + (int64_t)B * T * C + base;
-    S *x = xt + base;
-    if (apply_cfg <= 0) {
-        // no CFG (vt is [B,T,C]) or outside the CFG interval (vt = cond)
-        for (int t = tid; t < T; t += NTH) {
-            const int64_t i = (int64_t)t * C;
-            float c8[8], x8[8];
-            ld8(cond + i, c8);
-            if (out_mode) { st8(x + i, c8); continue; }
-            ld8(x + i, x8);
+    const int t = ch * APG_TC + tid;
+    const int64_t base = (int64_t)b * T * C + cg * CG, i = base + (int64_t)t * C;
+    const S *cond = vt, *unc = vt + (int64_t)B * T * C;
+    ApgPart *pp = part + (int64_t)(b * CG + cg) * nch;
+    float sf[8];
+    double denom[8], dot[8];
+    if (PHASE > 1) {
+        apg_totals<PHASE>(pp, nch, sf, denom, dot);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x8[j] = R<S>(x8[j] - R<S>(c8[j] * dt));
-            st8(x + i, x8);
+        for (int j = 0; j < 8; ++j) {
+            const float nrm = R<S>(sqrtf(sf[j]));
+            sf[j] = fminf(1.0f, R<S>(2.5f / nrm));
+            denom[j] = fmax(sqrt(denom[j]), 1e-12);
         }
-        return;
     }
-    S *rab = ra + base;
     float ss[8];
     double cs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ss[j] = 0.f; cs[j] = 0.0; }
-    for (int t = tid; t < T; t += NTH) {
-        const int64_t i = (int64_t)t * C;
-        float c8[8], u8[8], r8[8];
+    if (t < T) {
+        float c8[8], r8[8];
         ld8(cond + i, c8);
-        ld8(unc + i, u8);
-        if (!first_step) ld8(rab + i, r8);
+        if (PHASE == 1) {
+            float u8[8];
+            ld8(unc + i, u8);
+            if (!first_step) ld8(ra + i, r8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float diff = R<S>(c8[j] - u8[j]);
-            r8[j] = first_step ? diff : R<S>(diff + R<S>(-0.75f * r8[j]));
-            ss[j] += r8[j] * r8[j];
-            cs[j] += (double)c8[j] * (double)c8[j];
+            for (int j = 0; j < 8; ++j) {
+                const float diff = R<S>(c8[j] - u8[j]);
+                r8[j] = first_step ? diff : R<S>(diff + R<S>(-0.75f * r8[j]));
+                ss[j] = r8[j] * r8[j];
+                cs[j] = (double)c8[j] * (double)c8[j];
+            }
+            st8(ra + i, r8);
+        } else if (PHASE == 2) {
+            ld8(ra + i, r8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cs[j] = (double)R<S>(r8[j] * sf[j]) * ((double)c8[j] / denom[j]);
+        } else {
+            float x8[8];
+            ld8(ra + i, r8);
+            if (!out_mode) ld8(xt + i, x8);
+            const float gm1 = guidance - 1.0f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const double v0 = (double)R<S>(r8[j] * sf[j]);
+                const double v1 = (double)c8[j] / denom[j];
+                const float orth = R<S>((float)(v0 - dot[j] * v1));
+                const float g = R<S>(c8[j] + R<S>(gm1 * orth));
+                x8[j] = out_mode ? g : R<S>(x8[j] - R<S>(g * dt));
+            }
+            st8(xt + i, x8);
         }
-        st8(rab + i, r8);
     }
-    // block reduction per channel
+    if (PHASE == 3) return;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        ss[j] = wave_sum(ss[j]);
+        if (PHASE == 1) ss[j] = wave_sum(ss[j]);
         cs[j] = wave_sum_d(cs[j]);
     }
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { s_ss[wave][j] = ss[j]; s_cs[wave][j] = cs[j]; }
     __syncthreads();
-    float sf[8];
-    double denom[8], dot[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    if (tid < 8) {
         float a = 0.f;
         double c = 0.0;
-        for (int w = 0; w < NW; ++w) { a += s_ss[w][j]; c += s_cs[w][j]; }
-        const float nrm = R<S>(sqrtf(a));
-        sf[j] = fminf(1.0f, R<S>(2.5f / nrm));
-        denom[j] = fmax(sqrt(c), 1e-12);
-        dot[j] = 0.0;
-    }
-    __syncthreads();
-    for (int t = tid; t < T; t += NTH) {
-        const int64_t i = (int64_t)t * C;
-        float c8[8], r8[8];
-        ld8(cond + i, c8);
-        ld8(rab + i, r8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dot[j] += (double)R<S>(r8[j] * sf[j]) * ((double)c8[j] / denom[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dot[j] = wave_sum_d(dot[j]);
-    if (lane == 0)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s_cs[wave][j] = dot[j];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        double d = 0.0;
-        for (int w = 0; w < NW; ++w) d += s_cs[w][j];
-        dot[j] = d;
-    }
-    const float gm1 = guidance - 1.0f;
-    for (int t = tid; t < T; t += NTH) {
-        const int64_t i = (int64_t)t * C;
-        float c8[8], r8[8], x8[8];
-        ld8(cond + i, c8);
-        ld8(rab + i, r8);
-        if (!out_mode) ld8(x + i, x8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const double v0 = (double)R<S>(r8[j] * sf[j]);
-            const double v1 = (double)c8[j] / denom[j];
-            const float orth = R<S>((float)(v0 - dot[j] * v1));
-            const float g = R<S>(c8[j] + R<S>(gm1 * orth));
-            x8[j] = out_mode ? g : R<S>(x8[j] - R<S>(g * dt));
+        for (int w = 0; w < NW; ++w) { a += s_ss[w][tid]; c += s_cs[w][tid]; }
+        if (PHASE == 1) {
+            pp[ch].ss[tid] = a;
+            pp[ch].cs[tid] = c;
+        } else {
+            pp[ch].dot[tid] = c;
         }
-        st8(x + i, x8);
     }
+}
+
+// outside the CFG interval (vt = cond) or without CFG: the Euler update alone
+template <class S>
+__global__ __launch_bounds__(APG_TC) void euler_rows_kernel(const S *__restrict__ vt, S *__restrict__ xt, int T,
+                                                          float dt, int out_mode) {
+    constexpr int C = 64;
+    const int t = blockIdx.y * APG_TC + threadIdx.x;
+    if (t >= T) return;
+    const int64_t i = (int64_t)blockIdx.z * T * C + blockIdx.x * 8 + (int64_t)t * C;
+    float c8[8], x8[8];
+    ld8(vt + i, c8);
+    if (out_mode) { st8(xt + i, c8); return; }
+    ld8(xt + i, x8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x8[j] = R<S>(x8[j] - R<S>(c8[j] * dt));
+    st8(xt + i, x8);
 }
 
 template <class S>
@@ -225,17 +262,45 @@ int adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, flo
     return 0;
 }
 
+static ApgPart *apg_workspace(size_t n) {
+    static std::map<int, std::pair<ApgPart *, size_t>> by_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    auto &e = by_dev[dev];
+    if (e.second < n) {
+        if (e.first) (void)hipFree(e.first);
+        e.first = nullptr;
+        e.second = 0;
+        if (hipMalloc(&e.first, n * sizeof(ApgPart)) != hipSuccess) return nullptr;
+        e.second = n;
+    }
+    return e.first;
+}
+
 int apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float guidance, float dt, int apply_cfg,
               int first_step, int out_mode, bool f32, hipStream_t s) {
     if (C != 64) return fail(-1, "apg_euler: C must be 64");
     if (B <= 0 || T <= 0) return 0;
-    const dim3 g(C / 8, B);
-    if (f32)
-        apg_euler_kernel<float><<<g, 512, 0, s>>>((const float *)vt, (float *)xt, (float *)ra, B, T, guidance, dt,
-                                                  apply_cfg, first_step, out_mode);
-    else
-        apg_euler_kernel<bf16_t><<<g, 512, 0, s>>>((const bf16_t *)vt, (bf16_t *)xt, (bf16_t *)ra, B, T, guidance, dt,
-                                                   apply_cfg, first_step, out_mode);
+    const int nch = (T + APG_TC - 1) / APG_TC;
+    const dim3 g(C / 8, nch, B);
+    if (apply_cfg <= 0) {
+        if (f32) euler_rows_kernel<float><<<g, APG_TC, 0, s>>>((const float *)vt, (float *)xt, T, dt, out_mode);
+        else euler_rows_kernel<bf16_t><<<g, APG_TC, 0, s>>>((const bf16_t *)vt, (bf16_t *)xt, T, dt, out_mode);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+    ApgPart *part = apg_workspace((size_t)B * (C / 8) * nch);
+    if (!part) return fail(-1, "apg_euler: workspace allocation failed");
+#define APG_PHASES(S_)                                                                                       \
+    apg_phase_kernel<S_, 1><<<g, APG_TC, 0, s>>>((const S_ *)vt, (S_ *)xt, (S_ *)ra, B, T, guidance, dt,     \
+                                                 first_step, out_mode, part);                               \
+    apg_phase_kernel<S_, 2><<<g, APG_TC, 0, s>>>((const S_ *)vt, (S_ *)xt, (S_ *)ra, B, T, guidance, dt,     \
+                                                 first_step, out_mode, part);                               \
+    apg_phase_kernel<S_, 3><<<g, APG_TC, 0, s>>>((const S_ *)vt, (S_ *)xt, (S_ *)ra, B, T, guidance, dt,     \
+                                                 first_step, out_mode, part)
+    if (f32) { APG_PHASES(float); }
+    else { APG_PHASES(bf16_t); }
+#undef APG_PHASES
     HIP_TRY(hipGetLastError());
     return 0;
 }
