@@ -223,7 +223,10 @@ int acehip_fsq_codes_from_indices(const int32_t *indices, int M, const int *leve
  * out_mode 0: xt = bf16(xt − bf16(v·dt)) (ODE);  out_mode 1: xt = v (the
  * guided velocity, for the caller's SDE branch, base:1968-1973).
  * dtype: ACEHIP_BF16 (every op rounded to bf16 as torch does) or ACEHIP_F32 (the
- * fp32 parity mode: the same chain unrounded) for vt / xt / ra. */
+ * fp32 parity mode: the same chain unrounded) for vt / xt / ra.
+ * The norms' chunk partials live in one library-owned workspace per device
+ * (allocated on first use): calls on different streams of one device must not
+ * overlap in time (one stream per device, as the drop-in backend uses). */
 int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C,
                              float guidance, float dt, int apply_cfg, int first_step,
                              int out_mode, int dtype, void *stream);
