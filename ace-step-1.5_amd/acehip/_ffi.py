@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libacehip.s
 
 ACEHIP_F32 = 0
 ACEHIP_BF16 = 1
+# include/acehip.h ACEHIP_VERSION this binding's signatures were written against
+ABI_VERSION = 300
 
 # every symbol include/acehip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -127,6 +129,10 @@ def lib():
                                "or __graft_entry__.build()")
         handle = ctypes.CDLL(LIB_PATH)
         _declare(handle)
+        v = handle.acehip_get_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"acehip: {LIB_PATH} has ABI version {v}, this binding expects "
+                               f"{ABI_VERSION} (include/acehip.h); rebuild the library")
         _LIB = handle
     return _LIB
 

@@ -12,6 +12,8 @@ Seams:
   * VAE    — ``handler.vae.decode(z).sample`` (``vae_decode_chunks.py:42,95``)
              and ``handler.vae.encode(x).latent_dist.sample()``
              (``vae_encode.py:65``): replaced by :class:`~acehip.vae.OobleckBackend`;
+             ``handler.tiled_encode`` (``vae_encode.py:15-82``: 30 s chunks, 2 s
+             overlap, per-chunk host offload) becomes ONE untiled encode;
              ``handler.tiled_decode`` (``vae_decode.py:16-85``, called at
              ``generate_music_decode.py:164``) becomes ONE untiled decode of the
              whole batch — the reference's overlap-discard windows (1.6x the useful
@@ -197,7 +199,10 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
         orig_tiled = getattr(handler, "tiled_decode", None)
 
         def tiled_decode(latents, chunk_size=None, overlap=64, offload_wav_to_cpu=None):
-            # vae_decode.py:16-85 contract: [B, 64, T] -> [B, 2, T*hop]; untiled here
+            # vae_decode.py:16-85 contract: [B, 64, T] -> [B, 2, T*hop]; untiled here.
+            # None resolves through the handler's policy as the reference does (:53-54)
+            if offload_wav_to_cpu is None and hasattr(handler, "_should_offload_wav_to_cpu"):
+                offload_wav_to_cpu = bool(handler._should_offload_wav_to_cpu())
             try:
                 return vb.tiled_decode(latents, chunk_size, overlap, offload_wav_to_cpu)
             except Exception as e:  # pragma: no cover
@@ -207,6 +212,20 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
                 return orig_tiled(latents, chunk_size=chunk_size, overlap=overlap,
                                   offload_wav_to_cpu=offload_wav_to_cpu)
         handler.tiled_decode = tiled_decode
+        orig_tiled_enc = getattr(handler, "tiled_encode", None)
+
+        def tiled_encode(audio, chunk_size=None, overlap=None, offload_latent_to_cpu=True):
+            # vae_encode.py:15-82 contract (batch_prep.py:70, conditioning_embed.py:58):
+            # ONE untiled encode instead of the 30 s chunk loop
+            try:
+                return vb.tiled_encode(audio, chunk_size, overlap, offload_latent_to_cpu)
+            except Exception as e:  # pragma: no cover
+                if not fallback or orig_tiled_enc is None:
+                    raise
+                log.warning("acehip tiled_encode failed (%s); falling back", e)
+                return orig_tiled_enc(audio, chunk_size=chunk_size, overlap=overlap,
+                                      offload_latent_to_cpu=offload_latent_to_cpu)
+        handler.tiled_encode = tiled_encode
         out["vae"] = vb
     return out
 

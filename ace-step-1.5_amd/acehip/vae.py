@@ -107,12 +107,15 @@ class OobleckBackend:
         SURVEY §8a a19) is inside the reference's 64-frame overlap, so its
         overlap-discard tiling equals an untiled decode; we decode untiled."""
         wav = self.decode_tensor(latents)
+        # None = keep on the device here; the install() wrapper resolves None through the
+        # handler's own policy first (_should_offload_wav_to_cpu, vae_decode.py:53-54)
         return wav.cpu() if offload_wav_to_cpu else wav
 
     def encode_tensor(self, wav: torch.Tensor, sample: bool = True,
                       generator: Optional[torch.Generator] = None,
                       eps: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """wav [B, 2, N] → latent [B, 64, N/hop] (mean + std·ε when sample)."""
+        """wav [B, 2, N] → latent [B, 64, N // hop] (mean + std·ε when sample); any
+        N >= hop (AutoencoderOobleck's strided convs floor the length at every stage)."""
         if not self.with_encoder:
             raise RuntimeError("acehip: VAE created without encoder")
         wav = wav.to(device=self.device, dtype=torch.bfloat16).contiguous()
@@ -126,6 +129,33 @@ class OobleckBackend:
         z = torch.empty(B, self.cfg.decoder_input_channels, T, device=self.device, dtype=torch.bfloat16)
         check(lib().acehip_vae_encode(self.h, ptr(wav), B, N, ptr(eps), ptr(z), stream_ptr()), "vae_encode")
         return z
+
+    def tiled_encode(self, audio: torch.Tensor, chunk_size: Optional[int] = None,
+                     overlap: Optional[int] = None, offload_latent_to_cpu: bool = True) -> torch.Tensor:
+        """Handler ``tiled_encode`` contract (vae_encode.py:15-82, called by
+        batch_prep.py:70 and conditioning_embed.py:58): audio [B, 2, N] or [2, N] →
+        ``latent_dist.sample()`` latents [B, 64, N // hop] (or [64, N // hop]) in the
+        VAE dtype, on the CPU when ``offload_latent_to_cpu`` (the reference default).
+
+        ONE untiled encode of the whole batch instead of the reference's 30 s chunks
+        with 2 s overlap (vae_encode_chunks.py:10-98, each chunk a separate encode and,
+        by default, a device→host copy): the encoder's receptive field is inside the
+        overlap, so the overlap-discard tiling computes the untiled mean
+        (tests/test_gpu_long.py windows); ``chunk_size`` / ``overlap`` are accepted and
+        ignored.  The Gaussian draw is one ``randn`` over the whole latent, where the
+        reference draws per chunk — the same distribution, as in its own
+        ``samples <= chunk_size`` branch."""
+        del chunk_size, overlap
+        was_2d = audio.dim() == 2
+        if was_2d:
+            audio = audio.unsqueeze(0)
+        if audio.dim() != 3 or audio.shape[1] != self.cfg.audio_channels:
+            raise ValueError(f"acehip tiled_encode: expected [B, {self.cfg.audio_channels}, N] audio, "
+                             f"got {tuple(audio.shape)}")
+        z = self.encode_tensor(audio, sample=True)
+        if was_2d:
+            z = z.squeeze(0)
+        return z.cpu() if offload_latent_to_cpu else z
 
     def encode(self, wav: torch.Tensor):
         """diffusers-style: ``.encode(x).latent_dist.sample()`` / ``.mode()``."""

@@ -14,6 +14,7 @@
 //   proj_out ConvT  [D][64][2]   → [2·64][D] so the GEMM output [S][128] is
 //            the de-patchified [2S][64] sequence in place
 //   scale_shift_tables of all layers contiguous → one modulation launch
+#include <unistd.h>
 #include <map>
 #include <cmath>
 #include <vector>
@@ -615,14 +616,14 @@ int acehip_dit_forward_step(acehip_dit *h, const void *xt, const void *ctx, int 
 // attention / row-add variants): a change re-captures the graph instead of replaying a
 // stale one
 static int knob_hash() {
-    static const char *const names[] = {"ACEHIP_ATTN_CUS", "ACEHIP_ATTN_PW", "ACEHIP_FUSE_ROWADD",
-                                        "ACEHIP_GEMM_HP128", "ACEHIP_GEMM_TAILSPLIT", "ACEHIP_GEMM_W4",
-                                        "ACEHIP_GEMM_W4S", "ACEHIP_SPLITK_FILL", "ACEHIP_SPLITK_STAGES"};
-    uint32_t h = 2166136261u;                      // FNV-1a over "name=value;" pairs
-    for (const char *n : names) {
-        const char *v = getenv(n);
-        for (const char *c : {n, "=", v ? v : "", ";"})
-            for (; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
+    // every ACEHIP_* variable of the environment (the kernels read their A/B knobs
+    // from getenv at launch time, e.g. ACEHIP_ATTN_PW_SPLIT in attention.hip), so a
+    // knob added anywhere in the library can never be missing from the graph key
+    uint32_t h = 2166136261u;                      // FNV-1a over the "NAME=value" entries
+    for (char **e = environ; e && *e; ++e) {
+        if (strncmp(*e, "ACEHIP_", 7) != 0) continue;
+        for (const char *c = *e; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
+        h = (h ^ (uint8_t)';') * 16777619u;
     }
     return (int)(h & 0x7fffffff);
 }
@@ -908,6 +909,11 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
     else if (epi == 0) g.epi = EPI_STORE;
     else return fail(ACEHIP_E_ARG, "gemm_ex: epilogue");
     if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
+    if (variant >= 100) {   // small-M A/B: 100 + mode (gemm_small)
+        g.ws = abi_gemm_ws();
+        g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
+        return gemm_small(g, variant - 100, (hipStream_t)stream);
+    }
     if (variant < 0) {   // production dispatch incl. split-K for small grids
         g.ws = abi_gemm_ws();
         g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;

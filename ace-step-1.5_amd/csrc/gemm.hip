@@ -293,6 +293,121 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a, int sp
     *(uint2 *)(out + (int64_t)m * ldo + q) = pack4(o);
 }
 
+// ---------------------------------------------------------------------------
+// Weight-streaming ("skinny") GEMM for M ≤ 128 rows per chunk: turbo / short songs
+// (M = Bc·S = 125 at 10 s turbo) where every projection is a read of W with a few
+// FLOPs per byte (SwiGLU at M = 125: 120 flop/B, far below the 312 flop/B ridge).
+// No LDS staging and no barrier in the main loop: each block owns BN = 16·NT columns
+// (an N-slab) and one K-range (split), its 4 waves take interleaved 32-deep K-steps
+// (wave w: steps w, w+4, ...), and every operand fragment goes straight from memory
+// to the MFMA's registers by buffer_load_dwordx4 (W fragment = 16 rows × 64 B, the
+// X fragment likewise): W is read exactly once chip-wide, X (≤ 0.5 MB at K = 2048)
+// from L2.  Rows past M read zeros (the buffer range check), so no clamping.  The
+// four waves' partial accumulators are summed through LDS and the block stores its
+// fp32 partial tile [split][M][N] (the split-K workspace layout); the caller's
+// splitk_epilogue_kernel sums the splits in order and applies the epilogue.
+// Block order: units (slab, split) with equal index mod 8 share an XCD, so with
+// splits = 8 every XCD's blocks read one K-slice of X (L2-resident); the row chunks
+// of one unit are 8 block ids apart (same XCD: the second chunk's W comes from L2).
+template <int MT, int NT, int D>
+__global__ __launch_bounds__(256, 1) void skinny_kernel(GemmArgs a, int kper, int splits, int nchunk) {
+    __shared__ f32x4 red[4][MT][NT][64];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform values made provably uniform (readfirstlane), so the buffer
+    // descriptors live in SGPRs and no load is wrapped in a waterfall loop (T20)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 15, q = lane >> 4;
+    const int U = gridDim.x / nchunk, L = blockIdx.x;
+    int u, chunk;
+    if ((U & 7) == 0) {
+        const int g = L / (8 * nchunk), rem = L % (8 * nchunk);
+        chunk = rem >> 3;
+        u = g * 8 + (rem & 7);
+    } else {
+        u = L % U;
+        chunk = L / U;
+    }
+    const int slab = u / splits, split = u % splits;
+    const int n0 = slab * 16 * NT, m0 = chunk * 16 * MT;
+    const int kb = split * kper, nst = (min(a.K, kb + kper) - kb) / 32;
+    const int spw = (nst - wave + 3) / 4;               // this wave's K-steps: wave + 4t, t < spw
+    auto uni_rsrc = [](const void *p, int64_t bytes) {
+        const uint64_t v = (uint64_t)p;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rx = uni_rsrc(a.A + (int64_t)m0 * a.lda, (int64_t)(a.M - m0) * a.lda * 2);
+    const __amdgpu_buffer_rsrc_t rw = uni_rsrc(a.W + (int64_t)n0 * a.ldw, (int64_t)16 * NT * a.ldw * 2);
+    const __amdgpu_buffer_rsrc_t rz = uni_rsrc(a.W, 0);   // every load out of range: zeros
+    int ox[MT], ow[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) ox[i] = ((16 * i + r) * (int)a.lda + q * 8) * 2;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) ow[j] = ((16 * j + r) * (int)a.ldw + q * 8) * 2;
+
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // K-step t of this wave into (x, w); past the wave's steps the zero descriptor
+    // is used, so the padded last step adds exact zeros (no branch around the MFMAs)
+    bf16x8 xs[D][MT], wsr[D][NT];
+    auto load = [&](bf16x8(&x)[MT], bf16x8(&w)[NT], int t) {
+        const bool ok = t < spw;
+        const int ko = __builtin_amdgcn_readfirstlane((kb + (wave + 4 * t) * 32) * 2);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+            w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ok ? rw : rz, ow[j], ko, 0));
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+            x[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ok ? rx : rz, ox[i], ko, 0));
+    };
+    // MFMAs by inline asm with the accumulators tied to AGPRs ("+a"): with the builtin,
+    // hipcc keeps them in VGPRs beside the operand buffers and shuffles ~200 registers
+    // through v_accvgpr_* every iteration
+    auto mma = [&](const bf16x8(&x)[MT], const bf16x8(&w)[NT]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(w[j]), "v"(x[i]));
+    };
+    // D-slot register ring: D−1 K-steps in flight while one is multiplied
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) load(xs[d], wsr[d], d);
+    const int niter = (spw + D - 1) / D;
+    for (int it = 0; it < niter; ++it) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int t = it * D + d;
+            if (t + D - 1 < niter * D) load(xs[(d + D - 1) % D], wsr[(d + D - 1) % D], t + D - 1);
+            mma(xs[d], wsr[d]);
+        }
+    }
+    // XDL write → VALU (v_accvgpr_read) hazard: hipcc does not pad after asm MFMAs
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    // sum the four waves' partials: every wave parks its accumulators, then wave w
+    // reduces the (i, j) sub-tiles with (i·NT + j) % 4 == w and stores them
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) red[wave][i][j][lane] = acc[i][j];
+    __syncthreads();
+    float *ws = (float *)a.ws + (size_t)split * a.M * a.N;
+#pragma unroll
+    for (int t = 0; t < MT * NT; ++t) {
+        if (t % 4 != wave) continue;
+        const int i = t / NT, j = t % NT;
+        const f32x4 v = red[0][i][j][lane] + red[1][i][j][lane] + red[2][i][j][lane] + red[3][i][j][lane];
+        const int m = m0 + 16 * i + r;
+        if (m < a.M) *(f32x4 *)(ws + (int64_t)m * a.N + n0 + 16 * j + 4 * q) = v;
+    }
+}
+
 // Head-post epilogue of a BM×256 QKV tile (two 128-column heads): bf16(acc) → LDS tile
 // [BM][PITCH] (the operand ring is dead; store_acc(st, PITCH) writes the wave's
 // accumulators), then one 16-lane group per (row, head): RMSNorm + RoPE + head-major
@@ -933,6 +1048,47 @@ static int splitk_fill() {
     return e ? std::max(1, atoi(e)) : 1;
 }
 
+static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipStream_t s);
+
+// Skinny path (M ≤ 256, K % 128 == 0, N % 64 == 0): skinny_kernel<8, 4> over
+// ⌈M/128⌉ row chunks × N/64 slabs × `splits` K-ranges, splits chosen so the grid is
+// about one block per CU (K-steps per wave ≥ 2), then the split-K epilogue.
+// ACEHIP_SKINNY=0 disables it (the 128×128 split-K path then runs).
+static bool use_skinny() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_SKINNY");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+static int skinny_depth() {   // register-ring depth (A/B knob ACEHIP_SKINNY_D = 2 | 3 | 4)
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ACEHIP_SKINNY_D");
+        v = e ? atoi(e) : 3;
+    }
+    return v;
+}
+static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0) {
+    constexpr int MT = 8, NT = 4, BN = 16 * NT;
+    if (!depth) depth = skinny_depth();
+    const int cus = num_cus();
+    const int nchunk = (a.M + 16 * MT - 1) / (16 * MT);
+    const int slabs = a.N / BN, nk = a.K / 128;         // K in units of 4 waves × 32
+    int splits = std::max(1, (int)((cus + slabs * nchunk / 2) / (slabs * nchunk)));
+    splits = std::min(splits, std::max(1, nk / 2));
+    const int kper = ((nk + splits - 1) / splits) * 128;
+    splits = (a.K + kper - 1) / kper;
+    const size_t need = (size_t)splits * a.M * a.N * 4 + (a.epi == EPI_HEADPOST ? (size_t)a.M * a.N * 2 : 0);
+    if (need > a.ws_bytes) return 1;
+    if (depth == 4) skinny_kernel<MT, NT, 4><<<slabs * splits * nchunk, 256, 0, s>>>(a, kper, splits, nchunk);
+    else if (depth == 2) skinny_kernel<MT, NT, 2><<<slabs * splits * nchunk, 256, 0, s>>>(a, kper, splits, nchunk);
+    else skinny_kernel<MT, NT, 3><<<slabs * splits * nchunk, 256, 0, s>>>(a, kper, splits, nchunk);
+    HIP_TRY(hipGetLastError());
+    return splitk_finish(a, a, splits, s);
+}
+
 static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
     GemmArgs p = a;
     const int nk = a.K / BK;
@@ -942,6 +1098,12 @@ static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
     if (splitk_stages(a.N) == 3) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     HIP_TRY(hipGetLastError());
+    return splitk_finish(a, p, splits, s);
+}
+
+// sum the fp32 split partials in order + the GEMM's epilogue (head-post: staged bf16
+// projection + the standalone head_post kernel)
+static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipStream_t s) {
     bf16_t *out = a.C;
     int64_t ldo = a.ldc;
     if (a.epi == EPI_HEADPOST) {   // bf16 projection staged after the partials
@@ -992,6 +1154,22 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     return gemm_variant(tl, tv, s);
 }
 
+// small-M A/B entry (tools/bench_skinny.py): mode 2..4 = the skinny kernel at that ring
+// depth, 0 = the 128×128 split-K path; needs a.ws
+int gemm_small(const GemmArgs &a, int mode, hipStream_t s) {
+    if (!a.ws || a.M > 256 || a.N % 64 || a.K % 128) return fail(-1, "gemm_small: shape / workspace");
+    if (mode >= 2 && mode <= 4) {
+        const int rc = gemm_skinny(a, s, mode);
+        return rc == 1 ? fail(-1, "gemm_small: workspace too small") : rc;
+    }
+    const int cus = num_cus();
+    const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
+    const int nk = a.K / BK;
+    const int splits = (int)std::max<int64_t>(2, std::min<int64_t>(std::min<int64_t>(16, nk / 4),
+                                                                   (splitk_fill() * cus + tiles - 1) / tiles));
+    return gemm_splitk(a, splits, s);
+}
+
 int gemm(const GemmArgs &a, hipStream_t s) {
     if (a.M <= 0) return 0;
     // argument checks shared by every path (split-K included)
@@ -1006,6 +1184,11 @@ int gemm(const GemmArgs &a, hipStream_t s) {
         if (a.N % 256 || h.S <= 0 || (int64_t)h.B * h.S != a.M || (h.nq + h.nk + h.nv) * 128 != a.N ||
             h.S_dst < h.S || (h.nq && !h.qw) || (h.nk && !h.kw) || (h.cos == nullptr) != (h.sin == nullptr))
             return fail(-1, "gemm: head-post arguments inconsistent with the GEMM shape");
+    }
+    if (a.ws && a.M <= 256 && a.N % 64 == 0 && a.K % 128 == 0 && a.K >= 512 && use_skinny() &&
+        (a.epi != EPI_SWIGLU || a.N % 64 == 0)) {
+        const int rc = gemm_skinny(a, s);
+        if (rc <= 0) return rc;   // done (0) or failed (< 0); 1 = workspace too small
     }
     if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
         const int cus = num_cus();

@@ -45,6 +45,7 @@ constexpr int EPI_PARTIAL = 5;
 constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace      // internal: store the fp32 accumulators of split blockIdx.y to ws
 int gemm(const GemmArgs &a, hipStream_t s);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
+int gemm_small(const GemmArgs &a, int mode, hipStream_t s);        // small-M A/B (needs ws)
 
 // --------------------------------------------------------------- small ops --
 // y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16

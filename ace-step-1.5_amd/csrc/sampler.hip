@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 #include <map>
+#include <mutex>
 
 namespace acehip {
 namespace {
@@ -262,11 +263,16 @@ int adg_euler(const void *vt, void *xt, int B, int T, int C, float guidance, flo
     return 0;
 }
 
-static ApgPart *apg_workspace(size_t n) {
-    static std::map<int, std::pair<ApgPart *, size_t>> by_dev;
+// Chunk partials of the APG norms: one buffer per (device, stream), so calls on different
+// streams (or from different host threads, each on its own stream) never share scratch;
+// the map is guarded.  A buffer only grows (hipFree waits for the device first).
+static ApgPart *apg_workspace(size_t n, hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<ApgPart *, size_t>> by_key;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    auto &e = by_dev[dev];
+    std::lock_guard<std::mutex> lk(mu);
+    auto &e = by_key[{dev, s}];
     if (e.second < n) {
         if (e.first) (void)hipFree(e.first);
         e.first = nullptr;
@@ -289,7 +295,7 @@ int apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C, float gui
         HIP_TRY(hipGetLastError());
         return 0;
     }
-    ApgPart *part = apg_workspace((size_t)B * (C / 8) * nch);
+    ApgPart *part = apg_workspace((size_t)B * (C / 8) * nch, s);
     if (!part) return fail(-1, "apg_euler: workspace allocation failed");
 #define APG_PHASES(S_)                                                                                       \
     apg_phase_kernel<S_, 1><<<g, APG_TC, 0, s>>>((const S_ *)vt, (S_ *)xt, (S_ *)ra, B, T, guidance, dt,     \

@@ -149,10 +149,9 @@ int make_res(acehip_vae *h, const std::string &p, int C, int dil, ResU &r) {
     return 0;
 }
 
-// one implicit-GEMM conv launch
-const bf16_t *g_zero_page = nullptr;   // set per call from the handle (single-threaded per handle)
-
-int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps, int dil, int a_stride,
+// one implicit-GEMM conv launch; `zero` = the caller's zero page (the handle's own, so two
+// handles on different devices or threads never share launch state)
+int run_conv(const bf16_t *zero, const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps, int dil, int a_stride,
              int a_off, int c_stride, int c_off, int64_t L_out, bf16_t *out, bf16_t *out_s, const SnakeP *sn,
              const bf16_t *res, int phases, hipStream_t s) {
     ConvArgs a{};
@@ -162,12 +161,12 @@ int run_conv(const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps
     a.sa = sn ? sn->a : nullptr; a.sib = sn ? sn->ib : nullptr;
     a.res = res; a.L_out = L_out; a.N = c.cout; a.M = M;
     a.taps = taps; a.dil = dil; a.a_stride = a_stride; a.a_off = a_off; a.c_stride = c_stride; a.c_off = c_off;
-    a.zero = g_zero_page;
+    a.zero = zero;
     return conv_gemm(a, phases, s);
 }
 
 // residual unit on (x raw in X, x_s in cur): leaves x in X (if keep_raw) and next-snaked x in cur
-int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, const SnakeP &next, bool keep_raw,
+int res_unit(const bf16_t *zero, const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, const SnakeP &next, bool keep_raw,
              hipStream_t s) {
     int rc;
     if (r.c1.cin == 128) {
@@ -177,7 +176,7 @@ int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, co
         a.in = cur; a.L_in = L; a.Cin = 128; a.W = r.c1.Wp; a.bias = r.c1.bias;
         a.sa = r.s2.a; a.sib = r.s2.ib; a.L_out = L; a.N = 128; a.M = L;
         a.taps = 7; a.dil = r.dil; a.a_stride = 1; a.a_off = -3 * r.dil; a.c_stride = 1; a.c_off = 0;
-        a.zero = g_zero_page;
+        a.zero = zero;
         u.W2 = r.c2.Wp; u.W2p = r.W2p; u.b2 = r.c2.bias; u.x = X; u.out_s = other;
         u.in_zero_pad = 1;   // cur is h->P or h->Q
         u.sa_next = next.a; u.sib_next = next.ib; u.keep_raw = keep_raw ? 1 : 0;
@@ -185,9 +184,9 @@ int res_unit(const ResU &r, int64_t L, bf16_t *X, bf16_t *cur, bf16_t *other, co
         // the snaked output is in `other`: copy-free hand-back by swapping roles is done by the caller
         return 1;   // signals "output in other"
     }
-    if ((rc = run_conv(r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s)))
+    if ((rc = run_conv(zero, r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s)))
         return rc;
-    return run_conv(r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
+    return run_conv(zero, r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
 }
 
 }  // namespace
@@ -366,7 +365,6 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
     if (B <= 0 || T <= 0 || T > h->cfg.max_T) return fail(ACEHIP_E_ARG, "vae_decode: T out of range");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    g_zero_page = h->zero;
     const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels;
     const int64_t Lout = (int64_t)T * h->hop;
     int rc;
@@ -376,21 +374,21 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
         bf16_t *X = h->X, *cur = h->P, *other = h->Q;
         if ((rc = cf_to_nlc(zb, Cz, T, X, s))) return rc;
         // conv1 (k7) → snaked by block 0's snake1
-        if ((rc = run_conv(h->dconv1, X, T, T, 7, 1, 1, -3, 1, 0, T, nullptr, cur, &h->dec[0].snake, nullptr, 1, s)))
+        if ((rc = run_conv(h->zero, h->dconv1, X, T, T, 7, 1, 1, -3, 1, 0, T, nullptr, cur, &h->dec[0].snake, nullptr, 1, s)))
             return rc;
         int64_t L = T;
         for (int j = 0; j < n; ++j) {
             const auto &bk = h->dec[j];
             const int st = bk.stride, pad = (st + 1) / 2;
             // ConvTranspose1d as `st` phase GEMMs → raw x (residual) + snaked x for res_unit1
-            if ((rc = run_conv(bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
+            if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
                                nullptr, st, s)))
                 return rc;
             L *= st;
             std::swap(cur, other);
             for (int u = 0; u < 3; ++u) {
                 const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : (j + 1 < n ? h->dec[j + 1].snake : h->dsnake);
-                rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s);
+                rc = res_unit(h->zero, bk.res[u], L, X, cur, other, next, u < 2, s);
                 if (rc == 1) std::swap(cur, other);
                 else if (rc) return rc;
             }
@@ -403,11 +401,13 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
 int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *eps, void *z_out, void *stream) {
     if (!h || !wav || !z_out) return fail(ACEHIP_E_ARG, "null argument");
     if (!h->finalized || !h->cfg.with_encoder) return fail(ACEHIP_E_STATE, "vae_encode: encoder not loaded");
-    if (B <= 0 || N <= 0 || N % h->hop || N / h->hop > h->cfg.max_T)
-        return fail(ACEHIP_E_ARG, "vae_encode: N must be a positive multiple of hop within max_T");
+    // any N >= hop: every strided conv (k = 2s, pad ceil(s/2)) maps L to floor(L / s), so the
+    // latent length is floor(N / hop) as in AutoencoderOobleck.encode; the samples past
+    // hop·floor(N / hop) still feed the last frames through the convs' right halo
+    if (B <= 0 || N < h->hop || (int64_t)N > (int64_t)h->cfg.max_T * h->hop)
+        return fail(ACEHIP_E_ARG, "vae_encode: N must be in [hop, max_T * hop]");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    g_zero_page = h->zero;
     const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels, T = N / h->hop;
     int rc;
     for (int b = 0; b < B; ++b) {
@@ -423,20 +423,20 @@ int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *
             const auto &bk = h->enc[j];
             for (int u = 0; u < 3; ++u) {
                 const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : bk.snake;
-                rc = res_unit(bk.res[u], L, X, cur, other, next, u < 2, s);
+                rc = res_unit(h->zero, bk.res[u], L, X, cur, other, next, u < 2, s);
                 if (rc == 1) std::swap(cur, other);
                 else if (rc) return rc;
             }
             const int st = bk.stride, pad = (st + 1) / 2;
             const SnakeP &next = j + 1 < n ? h->enc[j + 1].res[0].s1 : h->esnake;
-            if ((rc = run_conv(bk.conv, cur, L, L / st, 2 * st, 1, st, -pad, 1, 0, L / st, j + 1 < n ? X : nullptr,
+            if ((rc = run_conv(h->zero, bk.conv, cur, L, L / st, 2 * st, 1, st, -pad, 1, 0, L / st, j + 1 < n ? X : nullptr,
                                other, &next, nullptr, 1, s)))
                 return rc;
             L /= st;
             std::swap(cur, other);
         }
         // conv2 (k3, pad 1) → h [T][2·Cz] (mean | scale), then the Gaussian sample
-        if ((rc = run_conv(h->econv2, cur, L, L, 3, 1, 1, -1, 1, 0, L, X, nullptr, nullptr, nullptr, 1, s))) return rc;
+        if ((rc = run_conv(h->zero, h->econv2, cur, L, L, 3, 1, 1, -1, 1, 0, L, X, nullptr, nullptr, nullptr, 1, s))) return rc;
         if ((rc = gauss_sample(X, T, Cz, eb, zb, s))) return rc;
     }
     return 0;
@@ -457,8 +457,13 @@ struct Tmp {   // scratch for the parity hooks, freed on scope exit (after a str
     }
 };
 const bf16_t *hook_zero_page() {
-    static bf16_t *z = nullptr;
-    if (!z && hipMalloc(&z, 4096) == hipSuccess && hipMemset(z, 0, 4096) != hipSuccess) z = nullptr;
+    // one zero page for the unit hooks, created once (thread-safe static init)
+    static bf16_t *const z = [] {
+        bf16_t *p = nullptr;
+        if (hipMalloc(&p, 4096) != hipSuccess) return (bf16_t *)nullptr;
+        if (hipMemset(p, 0, 4096) != hipSuccess) return (bf16_t *)nullptr;
+        return p;
+    }();
     return z;
 }
 }  // namespace
@@ -472,8 +477,8 @@ int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void 
     if ((kind == 0 && (k % 2 == 0 || stride != 1)) || (kind > 0 && k != 2 * stride) || (kind == 2 && L_in % stride))
         return fail(ACEHIP_E_ARG, "vae_conv: kernel / stride inconsistent with the kind");
     hipStream_t s = (hipStream_t)stream;
-    g_zero_page = hook_zero_page();
-    if (!g_zero_page) return fail(ACEHIP_E_OOM, "vae_conv: zero page");
+    const bf16_t *zero = hook_zero_page();
+    if (!zero) return fail(ACEHIP_E_OOM, "vae_conv: zero page");
     Tmp t;
     ConvL c;
     c.cin = Cin; c.cout = Cout; c.k = k; c.stride = stride; c.transposed = kind == 1;
@@ -494,10 +499,10 @@ int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void 
     bf16_t *o = (bf16_t *)out, *os = (bf16_t *)out_s;
     const bf16_t *x = (const bf16_t *)in, *r = (const bf16_t *)res;
     const int pad = (stride + 1) / 2;
-    if (kind == 0) rc = run_conv(c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s);
+    if (kind == 0) rc = run_conv(zero, c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s);
     else if (kind == 1)
-        rc = run_conv(c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s);
-    else rc = run_conv(c, x, L_in, L_in / stride, k, 1, stride, -pad, 1, 0, L_in / stride, o, os, snp, r, 1, s);
+        rc = run_conv(zero, c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s);
+    else rc = run_conv(zero, c, x, L_in, L_in / stride, k, 1, stride, -pad, 1, 0, L_in / stride, o, os, snp, r, 1, s);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     return 0;
@@ -510,8 +515,8 @@ int acehip_vae_resunit(const void *x, const void *x_s, int64_t L, int C, int dil
         return fail(ACEHIP_E_ARG, "vae_resunit: null argument");
     if (C != 128 || L <= 0 || dil < 1 || dil > 9) return fail(ACEHIP_E_ARG, "vae_resunit: C = 128, dilation 1..9");
     hipStream_t s = (hipStream_t)stream;
-    g_zero_page = hook_zero_page();
-    if (!g_zero_page) return fail(ACEHIP_E_OOM, "vae_resunit: zero page");
+    const bf16_t *zero = hook_zero_page();
+    if (!zero) return fail(ACEHIP_E_OOM, "vae_resunit: zero page");
     Tmp t;
     // the decoder's activation layout: kActPadRows zero rows in front, addressable rows behind
     const size_t rowb = (size_t)C * 2, pad = (size_t)kActPadRows * 2048 * 2;
@@ -542,7 +547,7 @@ int acehip_vae_resunit(const void *x, const void *x_s, int64_t L, int C, int dil
     if ((rc = permute_k1_weight(r.c2.Wp, r.W2p, C, s))) return rc;
     if ((rc = snake_params((const bf16_t *)alpha2, (const bf16_t *)beta2, C, r.s2.a, r.s2.ib, s))) return rc;
     if ((rc = snake_params((const bf16_t *)alpha_n, (const bf16_t *)beta_n, C, nx.a, nx.ib, s))) return rc;
-    rc = res_unit(r, L, xr, cur, other, nx, x_out != nullptr, s);
+    rc = res_unit(zero, r, L, xr, cur, other, nx, x_out != nullptr, s);
     if (rc < 0 || rc > 1) return rc;
     HIP_TRY(hipMemcpyAsync(xs_out, rc == 1 ? other : cur, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));
     if (x_out) HIP_TRY(hipMemcpyAsync(x_out, xr, (size_t)L * rowb, hipMemcpyDeviceToDevice, s));

@@ -67,8 +67,8 @@ def parse():
     p.add_argument("--repaint-start", type=float, default=60.0)
     p.add_argument("--repaint-end", type=float, default=120.0)
     p.add_argument("--text-len", type=int, default=128)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    p.add_argument("--pmc-derived-json", default=os.path.join(REPO, "profiles", "pmc_derived.json"))
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_roofline.json"),
+                   help="counter passes of the roofline kernel (tools/pmc_roofline.py), spliced in LABELLED")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU ranks over gloo with a stand-in song: exercises the launcher / timing / "
                         "max-over-ranks / JSON path without a GPU")
@@ -331,7 +331,9 @@ def main():
             # vae.encode(x).latent_dist.sample() (vae_encode.py:65), then the repaint source:
             # encoded target with silence inside the span + chunk mask of the span
             # (conditioning_masks.py:67-83)
-            z = vae.encode_tensor(src_wav, sample=True).transpose(1, 2)
+            # through the handler seam as the reference calls it (batch_prep.py:63-76:
+            # tiled_encode(audio, offload_latent_to_cpu=True) → .to(device) → transpose)
+            z = vae.tiled_encode(src_wav, offload_latent_to_cpu=True).to(dev).transpose(1, 2)
             src_r = z.clone()
             src_r[:, span[0]:span[1]] = src[:, span[0]:span[1]]
             cond_kw.update(src_latents=src_r.contiguous(), chunk_masks=span_mask)
@@ -383,14 +385,6 @@ def main():
     sw_flops = 2.0 * M * (2 * cfg.intermediate_size) * cfg.hidden_size
     sw_ms = ms_sw / max(n_sw, 1)
     sw_tflops = sw_flops / (sw_ms * 1e-3) / 1e12 if n_sw else None
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tr = json.load(f)
-        if tr.get("gemm_swiglu_M") == M:          # measured on this exact GEMM shape
-            traffic = tr.get("gemm_swiglu_hbm_bytes_per_launch")
-    except Exception:
-        pass
     # algorithmic bytes of one SwiGLU call: A [M][K] + W [N][K] in, C [M][N/2] out (bf16)
     sw_N, sw_K = 2 * cfg.intermediate_size, cfg.hidden_size
     sw_bytes = 2.0 * (M * sw_K + sw_N * sw_K + M * sw_N // 2)
@@ -404,18 +398,25 @@ def main():
         roofline = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1) if gbs else None,
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4) if gbs else None,
                     "algorithmic_bytes": sw_bytes}
-    roofline.update({"avg_launch_us": round(sw_ms * 1e3, 1), "launches": n_sw, "traffic": traffic})
-    # MFMA-busy counter and effective clock of the roofline kernel's main launch, from the
-    # committed counter pass of this shape (tools/gpu_prof.sh → tools/pmc_derived.py):
-    # frac above prices against the 2.4 GHz peak, frac_at_clock against the clock the chip held
+    roofline.update({"avg_launch_us": round(sw_ms * 1e3, 1), "launches": n_sw, "traffic": None})
+    # HBM traffic (FETCH_SIZE / WRITE_SIZE) and MFMA-busy / clock (SQ / GRBM) of this kernel
+    # come from SEPARATE rocprofv3 --pmc passes (counters cannot be read inside this timed
+    # run); they are spliced in only for the same GEMM shape and labelled with the file
+    # they come from and the box / clock / tree they were measured on — never as this run's
+    # numbers (tools/pmc_roofline.py writes the file from the passes)
     try:
-        with open(args.pmc_derived_json) as f:
-            der = json.load(f).get("gemm_pp_kernel<256, 3> grid=516096") if M == 6000 else None
-        if der and sw_tflops:
-            clk = der.get("clock_GHz")
-            roofline.update({"mfma_busy_frac_pmc": der["mfma_busy_frac"], "clock_GHz_pmc": clk,
-                             "frac_at_clock": round(sw_tflops / (PEAK_BF16_TFLOPS * clk / 2.4), 4) if clk else None,
-                             "pmc_source": "profiles/pmc_derived.json"})
+        with open(args.pmc_json) as f:
+            pm = json.load(f)
+        sw = pm.get("gemm_swiglu") or {}
+        if sw.get("M") == M:
+            roofline["traffic"] = sw.get("hbm_bytes_per_call")
+            roofline["pmc_from"] = {
+                "file": os.path.relpath(args.pmc_json, REPO), "same_run": False,
+                "box": pm.get("box"), "git_head": pm.get("git_head"),
+                "clock_GHz": sw.get("clock_GHz"), "mfma_busy_frac": sw.get("mfma_busy_frac"),
+                "avg_us_in_pass": sw.get("avg_us"),
+                "note": "counter passes of the same kernel shape on the named box (separate runs); "
+                        "traffic = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE per call"}
     except Exception:
         pass
     kernels = {k: {"launches": n, "avg_us": (ms / n * 1e3 if n else None)} for k, (n, ms) in prof_all.items()}

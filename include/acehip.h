@@ -31,7 +31,11 @@
 extern "C" {
 #endif
 
-#define ACEHIP_VERSION 100
+/* 100: round-1 ABI.  200: dtype argument on acehip_dit_forward and the three sampler
+ * entry points, acehip_dit_cfg.fp32 (round 2).  300: acehip_vae_encode accepts any
+ * N in [hop, max_T*hop] (latents = floor(N/hop) frames).  Callers check
+ * acehip_get_version() == ACEHIP_VERSION before binding (acehip/_ffi.py does). */
+#define ACEHIP_VERSION 300
 
 enum acehip_status {
     ACEHIP_OK = 0,
@@ -224,9 +228,9 @@ int acehip_fsq_codes_from_indices(const int32_t *indices, int M, const int *leve
  * guided velocity, for the caller's SDE branch, base:1968-1973).
  * dtype: ACEHIP_BF16 (every op rounded to bf16 as torch does) or ACEHIP_F32 (the
  * fp32 parity mode: the same chain unrounded) for vt / xt / ra.
- * The norms' chunk partials live in one library-owned workspace per device
- * (allocated on first use): calls on different streams of one device must not
- * overlap in time (one stream per device, as the drop-in backend uses). */
+ * The norms' chunk partials live in a library-owned workspace per (device,
+ * stream), allocated on first use under a lock: concurrent calls on different
+ * streams are independent; calls on one stream are ordered by that stream. */
 int acehip_sampler_apg_euler(const void *vt, void *xt, void *ra, int B, int T, int C,
                              float guidance, float dt, int apply_cfg, int first_step,
                              int out_mode, int dtype, void *stream);
@@ -276,9 +280,12 @@ int acehip_vae_finalize(acehip_vae *h);
  * receptive field is < the reference's 64-frame overlap). */
 int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, void *stream);
 
-/* vae.encode(x).latent_dist.sample() (vae_encode.py:65)
- * wav: bf16 [B, 2, N] (N multiple of hop); eps: bf16 [B, 64, N/hop] or NULL
- * (NULL → the mean); z_out: bf16 [B, 64, N/hop]. */
+/* vae.encode(x).latent_dist.sample() (vae_encode.py:65) — and, untiled, the
+ * handler's tiled_encode (vae_encode.py:15-82: the encoder's receptive field is
+ * inside the reference's 2 s overlap, tiled == untiled).
+ * wav: bf16 [B, 2, N], hop <= N <= max_T*hop; T = floor(N/hop) latent frames
+ * (every strided conv maps L to floor(L/s), as AutoencoderOobleck's does);
+ * eps: bf16 [B, 64, T] or NULL (NULL → the mean); z_out: bf16 [B, 64, T]. */
 int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *eps,
                       void *z_out, void *stream);
 
@@ -336,8 +343,10 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
  * and tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
  * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage, 5: 256x256 2-stage,
  * 6: 192x256 2-stage, 7: 256x256 ping-pong, 8: 192x256 ping-pong; 3 and 5-8
- * need N % 256 == 0; -1: the production choice, including split-K for grids
- * that cannot fill half the chip) — tuning and tests. */
+ * need N % 256 == 0; -1: the production choice, including the weight-streaming
+ * kernel for M <= 256 and split-K for grids that cannot fill half the chip;
+ * 100 + d: the weight-streaming kernel with a d-deep register ring (d = 2..4),
+ * 100: the 128x128 split-K path — small-M A/B) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 

@@ -21,7 +21,7 @@ def test_header_symbols_exported():
     missing = [s for s in sorted(declared) if not hasattr(lib, s)]
     assert not missing, missing
     assert set(_ffi.EXPORTS) == declared
-    assert lib.acehip_get_version() == 100
+    assert lib.acehip_get_version() == 300 == _ffi.ABI_VERSION
 
 
 def test_error_paths_without_gpu():

@@ -108,8 +108,10 @@ def test_prepare_condition_dropin(gpu_device):
 @pytest.mark.parametrize("name", ["tiny_bfloat16", "tiny_float32"])
 def test_tokenizer_detokenizer_vs_reference(gpu_device, name):
     """AttentionPooler / tokenizer (+ restated FSQ) / detokenizer on libacehip vs the
-    reference fixtures (tools/make_golden.py gen_tokenizer); codes may flip at a rounding
-    boundary in bf16, so indices are compared by agreement rate."""
+    reference fixtures (tools/make_golden.py gen_tokenizer).  The HIP pooler's bf16 z differs
+    from the reference's by rounding, so a code can flip where z sits at a rounding
+    boundary: indices are compared here by agreement rate; on IDENTICAL z the quantizer is
+    bit-exact (test_fsq_bit_exact_exhaustive)."""
     from acehip.condition import AudioDetokenizer, AudioTokenizer
     from acehip.weights import synth_tokenizer_weights
     meta = golden_manifest()["tokenizer"][name]
@@ -139,6 +141,75 @@ def test_tokenizer_detokenizer_vs_reference(gpu_device, name):
     torch.cuda.synchronize()
     assert torch.equal(again, quant)
     tok.close(); det.close()
+
+
+def test_fsq_bit_exact_exhaustive(gpu_device):
+    """FSQ on IDENTICAL inputs is index work and must be bit-exact: the HIP
+    quantizer gets z in bf16 (the project_in GEMM output), so every one of the 65,280
+    finite bf16 values plus ±inf is fed in every level column ([8,8,8,5,5,5],
+    configuration_acestep_v15.py:152) and codes / indices must equal the restated
+    vector_quantize_pytorch FSQ (oracle/condenc_oracle.py, base:1196-1200).  The rows
+    are then rolled per column so each row mixes levels.  Rounding-boundary margin of
+    this input set (fp64 analysis, CPU): the nearest bounded value to a .5 tie is
+    4.9e-4 away — ~4000 fp32 ulps — so no tanh-ulp tie exists among bf16 inputs;
+    the count of mismatches is asserted to be 0.  Then the inverse: all
+    8·8·8·5·5·5 = 64,000 indices → codes equal the oracle, and codes → indices →
+    codes is the identity on the device."""
+    from acehip import _ffi as ff
+    bits = torch.arange(0, 65536, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    vals = bits[~torch.isnan(bits.float())]
+    assert vals.numel() == 65536 - 254
+    nl = len(co.FSQ_LEVELS)
+    zc = torch.stack([torch.roll(vals, 977 * i) for i in range(nl)], dim=1)      # [M, 6]
+    M = zc.shape[0]
+    z = torch.zeros(M, 128, dtype=torch.bfloat16)
+    z[:, :nl] = zc
+    z[:, nl:] = torch.randn(M, 128 - nl, generator=torch.Generator().manual_seed(3)).bfloat16()  # ignored
+    ref_codes, ref_idx = co.fsq_quantize(zc)
+    lv = (ff.c_int * nl)(*co.FSQ_LEVELS)
+    zd = z.to(gpu_device).contiguous()
+    codes = torch.full((M, 64), 7.0, device=gpu_device, dtype=torch.bfloat16)
+    idx = torch.empty(M, device=gpu_device, dtype=torch.int32)
+    ff.check(ff.lib().acehip_fsq_quantize(ff.ptr(zd), 128, M, lv, nl, ff.ptr(codes), 64, ff.ptr(idx),
+                                          ff.stream_ptr()), "fsq_quantize")
+    torch.cuda.synchronize()
+    c, i = codes.cpu(), idx.cpu()
+    mism = int((i != ref_idx).sum())
+    assert mism == 0, f"{mism} index mismatches"
+    assert torch.equal(c[:, :nl], ref_codes)
+    assert torch.equal(c[:, nl:], torch.zeros(M, 64 - nl, dtype=torch.bfloat16))   # K padding
+    # every index of the lattice -> codes (FSQ.indices_to_codes) and back
+    n_idx = 1
+    for L in co.FSQ_LEVELS:
+        n_idx *= L
+    all_idx = torch.arange(n_idx, dtype=torch.int32)
+    ref_c = co.fsq_codes_from_indices(all_idx, torch.bfloat16)
+    ad = all_idx.to(gpu_device)
+    c2 = torch.empty(n_idx, 64, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_fsq_codes_from_indices(ff.ptr(ad), n_idx, lv, nl, ff.ptr(c2), 64, ff.stream_ptr()),
+             "fsq_codes")
+    torch.cuda.synchronize()
+    assert torch.equal(c2[:, :nl].cpu(), ref_c)
+    hw = torch.tensor([L // 2 for L in co.FSQ_LEVELS])
+    basis = torch.cumprod(torch.tensor([1] + co.FSQ_LEVELS[:-1]), 0)
+    back = ((c2[:, :nl].cpu().float() * hw + hw) * basis).sum(-1).round().to(torch.int32)
+    assert torch.equal(back, all_idx)
+    # device round trip indices -> codes -> indices: quantize the bf16 pre-image of each
+    # lattice code under bound() (z = atanh((c·(L//2) + offset)/half_l) − shift)
+    L = torch.tensor(co.FSQ_LEVELS, dtype=torch.float64)
+    half = (L - 1) * (1 + 1e-3) / 2
+    off = torch.where(L % 2 == 0, 0.5, 0.0)
+    pre = torch.atanh((c2[:, :nl].cpu().double() * (L // 2) + off) / half) - torch.atanh(off / half)
+    zp = torch.zeros(n_idx, 128, dtype=torch.bfloat16)
+    zp[:, :nl] = pre.float().bfloat16()
+    zpd = zp.to(gpu_device)
+    idx2 = torch.empty(n_idx, device=gpu_device, dtype=torch.int32)
+    codes2 = torch.empty(n_idx, 64, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_fsq_quantize(ff.ptr(zpd), 128, n_idx, lv, nl, ff.ptr(codes2), 64, ff.ptr(idx2),
+                                          ff.stream_ptr()), "fsq_quantize")
+    torch.cuda.synchronize()
+    assert torch.equal(idx2.cpu(), all_idx)
+    assert torch.equal(codes2.cpu(), c2.cpu())
 
 
 def test_prepare_condition_cover(gpu_device):

@@ -231,6 +231,51 @@ def test_apg_euler_kernel_replay(gpu_device, name):
     assert rel_l2(out, ref) < 5e-3, (rel_l2(out, ref), worst)
 
 
+@pytest.mark.parametrize("T,dtype", [(6000, torch.bfloat16), (1001, torch.bfloat16), (6000, torch.float32),
+                                     (1001, torch.float32)])
+def test_apg_euler_multichunk(gpu_device, T, dtype):
+    """The APG step's per-(song, channel) norms over T are reduced across 256-row chunks in
+    three launches (csrc/sampler.hip): at production length (T = 6000: 24 chunks) and at a
+    ragged length (T = 1001: 4 chunks, the last one 233 rows), B = 2, CFG toggling on/off
+    and the first-step momentum reset, every step compared with the oracle's apg
+    (apg_guidance.py:16-56) + Euler (base:1975-1979) started from the device's own state
+    (xt, momentum buffer) so each step is checked on identical inputs."""
+    from acehip.dit import apg_euler_
+    B, C, guidance = 2, 64, 7.0
+    g = torch.Generator().manual_seed(T)
+    xt = torch.randn(B, T, C, generator=g).to(dtype)
+    ra = torch.zeros(B, T, C, dtype=dtype)
+    xd, rd = xt.to(gpu_device).contiguous(), ra.to(gpu_device).contiguous()
+    plan = [(1, 1), (1, 0), (0, 0), (1, 0), (1, 0)]        # (apply_cfg, first_step)
+    for step, (apply, first) in enumerate(plan):
+        vt = (torch.randn(2 * B, T, C, generator=g) * (1.0 + step)).to(dtype)
+        dt = float(torch.tensor(0.0371 * (step + 1), dtype=dtype))
+        x0, r0 = xd.cpu(), rd.cpu()
+        apg_euler_(vt.to(gpu_device).contiguous(), xd, rd, guidance, dt, apply, first)
+        torch.cuda.synchronize()
+        cond, uncond = vt.chunk(2)
+        if apply:
+            mom = sampler_oracle.Momentum()
+            mom.running_average = 0 if first else r0
+            v = sampler_oracle.apg(cond, uncond, guidance, mom, dims=(1,))
+            ref_r = mom.running_average
+        else:
+            v, ref_r = cond, r0
+        ref_x = x0 - v * torch.tensor(dt, dtype=dtype)
+        got_x, got_r = xd.cpu(), rd.cpu()
+        # the momentum update is elementwise: exact; the norms' reduction order differs from
+        # torch's, which can move a clip scale by an ulp -> a bf16 ulp of drift in a few elements
+        if dtype == torch.bfloat16:      # every op rounded to bf16: exact
+            assert torch.equal(got_r, ref_r.to(dtype)), step
+        else:                            # fp32: hipcc may contract the update into an FMA
+            assert rel_l2(got_r, ref_r) < 1e-6, step
+        tol = 2e-3 if dtype == torch.bfloat16 else 1e-5
+        r = rel_l2(got_x.float(), ref_x.float())
+        assert r < tol, (step, r)
+        frac = (got_x != ref_x).float().mean().item()
+        assert frac < (0.01 if dtype == torch.bfloat16 else 1.0), (step, frac)
+
+
 def test_schedule_bit_exact_on_device(gpu_device):
     from acehip.dit import base_schedule
     for steps, shift in ((8, 3.0), (27, 3.0), (60, 3.0), (10, 1.0)):
@@ -426,10 +471,14 @@ def test_weight_reload_matches_fresh_handle(gpu_device):
     a.close(); b.close()
 
 
-@pytest.mark.parametrize("M,N,K", [(125, 2048, 6144), (125, 12288, 2048), (250, 4096, 2048), (61, 256, 1024)])
+@pytest.mark.parametrize("M,N,K", [(125, 2048, 6144), (125, 12288, 2048), (250, 4096, 2048), (61, 256, 1024),
+                                   (1, 2048, 2048), (16, 4096, 2048), (128, 2048, 2048), (129, 2048, 6144),
+                                   (256, 12288, 2048), (200, 2048, 1088), (300, 2048, 2048)])
 def test_gemm_splitk_small_m(gpu_device, M, N, K):
-    """Split-K path for grids that cannot fill the chip (short songs / turbo): store,
-    residual and SwiGLU epilogues through the production dispatch (variant -1)."""
+    """Small-M paths (short songs / turbo) through the production dispatch (variant -1):
+    the weight-streaming skinny kernel (M ≤ 256, K % 128 == 0: one or two 128-row chunks,
+    rows past M read as zeros, 1–8 K splits) and the 128×128 split-K path (K % 128 != 0,
+    M > 256); store, residual and SwiGLU epilogues."""
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)

@@ -131,6 +131,14 @@ class StubHandler:
     def tiled_decode(self, latents, chunk_size=None, overlap=64, offload_wav_to_cpu=None):
         raise AssertionError("the reference tiled_decode ran")
 
+    def tiled_encode(self, audio, chunk_size=None, overlap=None, offload_latent_to_cpu=True):
+        raise AssertionError("the reference tiled_encode (30 s chunk loop) ran")
+
+    offload_policy = False
+
+    def _should_offload_wav_to_cpu(self):          # memory_utils.py:85-103
+        return self.offload_policy
+
     # LoRA lifecycle (handler/lora/lifecycle.py): adapters wrap decoder Linears
     def add_lora(self, path="synthetic", scale=1.0):
         dec = self.model.decoder
@@ -283,9 +291,38 @@ def test_install_drives_handler_calls(gpu_device, installed):
     assert torch.equal(h.vae.decode(z).sample, wav)                  # vae.decode seam too
     host = h.tiled_decode(z, offload_wav_to_cpu=True)
     assert host.device.type == "cpu" and torch.equal(host, wav.cpu())
+    # offload_wav_to_cpu=None resolves through the handler's own policy (vae_decode.py:53-54)
+    h.offload_policy = True
+    assert h.tiled_decode(z).device.type == "cpu"
+    h.offload_policy = False
+    assert h.tiled_decode(z).is_cuda
     # encode seam: vae.encode(x).latent_dist.sample() (vae_encode.py:65)
     m = h.vae.encode(wav[:1].bfloat16()).latent_dist.mode()
     assert m.shape == (1, 64, T)
+    # handler.tiled_encode (vae_encode.py:15-82) -> ONE untiled encode; the reference chunk loop
+    # never runs (the stub's tiled_encode raises).  B = 2, 3-D and 2-D input, a sample count
+    # that is not a multiple of hop, both offload settings; latent_dist.sample() semantics:
+    # mean + std * eps, checked against the untiled encode with the same eps draw.
+    vb = out["vae"]
+    n = T * 1920 + 777
+    g = torch.Generator(device=gpu_device).manual_seed(11)
+    audio = (0.3 * torch.randn(2, 2, n, device=gpu_device, generator=g)).float()
+    torch.manual_seed(5)
+    zc = h.tiled_encode(audio)                                  # reference default: offload
+    assert zc.device.type == "cpu" and zc.shape == (2, 64, T) and zc.dtype == torch.bfloat16
+    torch.manual_seed(5)
+    zg = h.tiled_encode(audio, offload_latent_to_cpu=False)
+    assert zg.is_cuda and torch.equal(zg.cpu(), zc)
+    torch.manual_seed(5)
+    eps = torch.randn(2, 64, T, device=gpu_device, dtype=torch.bfloat16)
+    direct = vb.encode_tensor(audio.bfloat16(), sample=True, eps=eps)
+    torch.cuda.synchronize()
+    assert torch.equal(zg, direct)
+    mean = vb.encode_tensor(audio.bfloat16(), sample=False)
+    assert not torch.equal(zg, mean)                             # a sample, not the mode
+    z1 = h.tiled_encode(audio[1], offload_latent_to_cpu=False)  # [2, N] -> [64, T]
+    assert z1.shape == (64, T)
+    torch.cuda.synchronize()
 
 
 def test_install_lora_repack_vs_oracle(gpu_device, installed):

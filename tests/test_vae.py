@@ -71,24 +71,81 @@ def test_vae_decode_parity(gpu_device, cfg_name, T):
     be.close()
 
 
+def test_oracle_encode_ragged_length():
+    """AutoencoderOobleck's strided convs (k = 2s, pad ceil(s/2)) floor the length at every
+    stage: N samples → floor(N / hop) latent frames, and the tail samples past
+    hop·floor(N / hop) still reach the last frame through the right halo."""
+    cfg = VAEConfig.tiny()
+    W = synth_vae_weights(cfg, seed=3, mode="parity", with_encoder=True)
+    g = torch.Generator().manual_seed(2)
+    wav = 0.3 * torch.randn(1, 2, 3 * 1920 + 1500, generator=g)
+    with torch.no_grad():
+        z = vae_oracle.encode_sample(W, cfg, wav)
+        zt = vae_oracle.encode_sample(W, cfg, wav[:, :, :3 * 1920])
+    assert z.shape == (1, 64, 3)
+    assert not torch.allclose(z[:, :, -1], zt[:, :, -1])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg_name", ["tiny", "full"])
-def test_vae_encode_parity(gpu_device, cfg_name):
+@pytest.mark.parametrize("cfg_name,extra,B", [("tiny", 0, 1), ("full", 0, 1), ("tiny", 777, 2),
+                                              ("full", 1919, 2)])
+def test_vae_encode_parity(gpu_device, cfg_name, extra, B):
+    """Encode parity vs the fp32 oracle, including sample counts that are not a multiple of
+    hop (the handler's tiled_encode seam takes raw source audio)."""
     cfg = VAEConfig.tiny() if cfg_name == "tiny" else VAEConfig()
     W = synth_vae_weights(cfg, seed=6, mode="parity", with_encoder=True)
     g = torch.Generator().manual_seed(1)
     T = 3
-    wav = (0.3 * torch.randn(1, 2, T * 1920, generator=g)).bfloat16()
-    eps = torch.randn(1, 64, T, generator=g).bfloat16()
+    wav = (0.3 * torch.randn(B, 2, T * 1920 + extra, generator=g)).bfloat16()
+    eps = torch.randn(B, 64, T, generator=g).bfloat16()
     with torch.no_grad():
         ref_mean = vae_oracle.encode_sample(W, cfg, wav.float())
         ref_s = vae_oracle.encode_sample(W, cfg, wav.float(), eps.float())
     be = _hip_vae(cfg, W, gpu_device, max_T=8)
     mean = be.encode_tensor(wav.to(gpu_device), sample=False).float().cpu()
     smp = be.encode_tensor(wav.to(gpu_device), eps=eps).float().cpu()
+    assert mean.shape == ref_mean.shape == (B, 64, T)
     assert rel_l2(mean, ref_mean) < 0.03, rel_l2(mean, ref_mean)
     assert rel_l2(smp, ref_s) < 0.03
     be.close()
+
+
+@pytest.mark.gpu
+def test_vae_two_handles_alternate(gpu_device):
+    """Launch state is per handle (each handle's own zero page goes into the conv
+    arguments): two handles with different weights, decoding alternately and from two
+    host threads, give exactly what each gives alone."""
+    import threading
+    cfg = VAEConfig.tiny()
+    bes = [_hip_vae(cfg, synth_vae_weights(cfg, seed=s, mode="parity", with_encoder=True), gpu_device, 8)
+           for s in (21, 22)]
+    g = torch.Generator().manual_seed(9)
+    zs = [torch.randn(1, 64, 6, generator=g).bfloat16().to(gpu_device) for _ in range(2)]
+    alone = []
+    for be, z in zip(bes, zs):
+        alone.append(be.decode_tensor(z))
+        torch.cuda.synchronize()
+    for _ in range(3):
+        for i in (1, 0):
+            o = bes[i].decode_tensor(zs[i])
+            torch.cuda.synchronize()
+            assert torch.equal(o, alone[i])
+    res = [None, None]
+
+    def run(i):
+        s = torch.cuda.Stream(device=gpu_device)
+        with torch.cuda.stream(s):
+            outs = [bes[i].decode_tensor(zs[i]) for _ in range(4)]
+        s.synchronize()
+        res[i] = all(torch.equal(o, alone[i]) for o in outs)
+    th = [threading.Thread(target=run, args=(i,)) for i in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert res == [True, True]
+    for be in bes:
+        be.close()
 
 
 @pytest.mark.gpu
