@@ -331,16 +331,20 @@ __global__ __launch_bounds__(256, 1) void skinny_kernel(GemmArgs a, int kper, in
     const int n0 = slab * 16 * NT, m0 = chunk * 16 * MT;
     const int kb = split * kper, nst = (min(a.K, kb + kper) - kb) / 32;
     const int spw = (nst - wave + 3) / 4;               // this wave's K-steps: wave + 4t, t < spw
-    auto uni_rsrc = [](const void *p, int64_t bytes) {
+    // buffer descriptors as SGPR quads (base, stride 0, num_records, gfx9 dword3),
+    // built from provably wave-uniform values
+    auto srd = [](const void *p, int64_t bytes) {
         const uint64_t v = (uint64_t)p;
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-        const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
-        return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+        u32x4 d;
+        d[0] = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        d[1] = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        d[2] = __builtin_amdgcn_readfirstlane((uint32_t)bytes);
+        d[3] = 0x00020000;
+        return d;
     };
-    const __amdgpu_buffer_rsrc_t rx = uni_rsrc(a.A + (int64_t)m0 * a.lda, (int64_t)(a.M - m0) * a.lda * 2);
-    const __amdgpu_buffer_rsrc_t rw = uni_rsrc(a.W + (int64_t)n0 * a.ldw, (int64_t)16 * NT * a.ldw * 2);
-    const __amdgpu_buffer_rsrc_t rz = uni_rsrc(a.W, 0);   // every load out of range: zeros
+    const u32x4 rx = srd(a.A + (int64_t)m0 * a.lda, (int64_t)(a.M - m0) * a.lda * 2);
+    const u32x4 rw = srd(a.W + (int64_t)n0 * a.ldw, (int64_t)16 * NT * a.ldw * 2);
+    const u32x4 rz = srd(a.W, 0);   // every load out of range: zeros
     int ox[MT], ow[NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) ox[i] = ((16 * i + r) * (int)a.lda + q * 8) * 2;
@@ -353,23 +357,27 @@ __global__ __launch_bounds__(256, 1) void skinny_kernel(GemmArgs a, int kper, in
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // K-step t of this wave into (x, w); past the wave's steps the zero descriptor
-    // is used, so the padded last step adds exact zeros (no branch around the MFMAs)
-    bf16x8 xs[D][MT], wsr[D][NT];
-    auto load = [&](bf16x8(&x)[MT], bf16x8(&w)[NT], int t) {
+    // K-step t of this wave into (x, w): inline-asm buffer loads, so the only vector-
+    // memory operations of the loop are these (MT + NT per step) and the waits below
+    // count them exactly (hipcc's own waitcnt placement drained the ring at the loop
+    // join); past the wave's steps the zero descriptor is used, so a padded step adds
+    // exact zeros with no branch around the loads or the MFMAs
+    u32x4 xs[D][MT], wsr[D][NT];
+    auto load = [&](u32x4(&x)[MT], u32x4(&w)[NT], int t) {
         const bool ok = t < spw;
+        const u32x4 sw = ok ? rw : rz, sx = ok ? rx : rz;
         const int ko = __builtin_amdgcn_readfirstlane((kb + (wave + 4 * t) * 32) * 2);
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-            w[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ok ? rw : rz, ow[j], ko, 0));
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(w[j]) : "v"(ow[j]), "s"(sw), "s"(ko));
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-            x[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ok ? rx : rz, ox[i], ko, 0));
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(x[i]) : "v"(ox[i]), "s"(sx), "s"(ko));
     };
     // MFMAs by inline asm with the accumulators tied to AGPRs ("+a"): with the builtin,
-    // hipcc keeps them in VGPRs beside the operand buffers and shuffles ~200 registers
+    // hipcc keeps them in VGPRs beside the operand ring and shuffles ~200 registers
     // through v_accvgpr_* every iteration
-    auto mma = [&](const bf16x8(&x)[MT], const bf16x8(&w)[NT]) {
+    auto mma = [&](const u32x4(&x)[MT], const u32x4(&w)[NT]) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -384,12 +392,23 @@ __global__ __launch_bounds__(256, 1) void skinny_kernel(GemmArgs a, int kper, in
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const int t = it * D + d;
-            if (t + D - 1 < niter * D) load(xs[(d + D - 1) % D], wsr[(d + D - 1) % D], t + D - 1);
+            load(xs[(d + D - 1) % D], wsr[(d + D - 1) % D], t + D - 1);
+            // slot d landed: only the D−1 younger steps' loads may still be in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (MT + NT)) : "memory");
             mma(xs[d], wsr[d]);
         }
     }
-    // XDL write → VALU (v_accvgpr_read) hazard: hipcc does not pad after asm MFMAs
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    // the ring's last (zero) loads land before their registers can be reused: hipcc does
+    // not know they are in flight, so the ring stays live (empty asm uses) until the wait;
+    // XDL write → VALU read (v_accvgpr_read) hazard: hipcc does not pad after asm MFMAs
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) asm volatile("" ::"v"(xs[d][i]));
+#pragma unroll
+        for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(wsr[d][j]));
+    }
     // sum the four waves' partials: every wave parks its accumulators, then wave w
     // reduces the (i, j) sub-tiles with (i·NT + j) % 4 == w and stores them
 #pragma unroll
@@ -1053,12 +1072,16 @@ static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipSt
 // Skinny path (M ≤ 256, K % 128 == 0, N % 64 == 0): skinny_kernel<8, 4> over
 // ⌈M/128⌉ row chunks × N/64 slabs × `splits` K-ranges, splits chosen so the grid is
 // about one block per CU (K-steps per wave ≥ 2), then the split-K epilogue.
-// ACEHIP_SKINNY=0 disables it (the 128×128 split-K path then runs).
+// Measured (tools/bench_skinny.py, cold weights, M = 16 / 64 / 125 / 250, one process):
+// no faster than the 128×128 split-K path — SwiGLU at M = 125 34 vs 26 µs, down 21 vs 20,
+// QKV 17 vs 18, O 16 vs 16; even W-only streaming (M = 16) reaches 2.4 TB/s against
+// split-K's 2.9, and every shape carries a ~10 µs floor (two launches, the cold-weight
+// first touch) — so it is off by default; ACEHIP_SKINNY=1 selects it (A/B).
 static bool use_skinny() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("ACEHIP_SKINNY");
-        v = (e && e[0] == '0') ? 0 : 1;
+        v = (e && e[0] == '1') ? 1 : 0;
     }
     return v == 1;
 }

@@ -3,7 +3,7 @@
 // Restates reference base:1943-1979 with apg_forward / MomentumBuffer /
 // project (acestep/models/base/apg_guidance.py:5-56):
 //   diff = cond − uncond; ra = diff + (−0.75)·ra            (bf16 ops)
-//   ‖ra‖₂ over T per channel → bf16; sf = min(1, bf16(2.5/‖ra‖)); v0 = bf16(ra·sf)
+//   ‖ra‖₂ over T per channel → bf16; sf = min(1, bf16(bf16(1/‖ra‖)·2.5)); v0 = bf16(ra·sf)
 //   v1 = cond/max(‖cond‖,1e-12); par = Σ(v0·v1)·v1; orth = v0 − par   (float64)
 //   vt = bf16(cond + bf16((g−1)·bf16(orth)));  xt = bf16(xt − bf16(vt·dt))
 // Storage type S = bf16 (production: every op output rounded to bf16 as torch
@@ -104,7 +104,10 @@ __global__ __launch_bounds__(APG_TC) void apg_phase_kernel(const S *__restrict__
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float nrm = R<S>(sqrtf(sf[j]));
-            sf[j] = fminf(1.0f, R<S>(2.5f / nrm));
+            // norm_threshold / diff_norm (apg_guidance.py:47) is a python float over a
+            // tensor: torch evaluates __rtruediv__ as reciprocal(diff_norm) * 2.5, each
+            // rounded to the tensor dtype — not bf16(2.5 / n) (differs for ~1 in 4 norms)
+            sf[j] = fminf(1.0f, R<S>(R<S>(1.0f / nrm) * 2.5f));
             denom[j] = fmax(sqrt(denom[j]), 1e-12);
         }
     }

@@ -269,11 +269,18 @@ def test_apg_euler_multichunk(gpu_device, T, dtype):
             assert torch.equal(got_r, ref_r.to(dtype)), step
         else:                            # fp32: hipcc may contract the update into an FMA
             assert rel_l2(got_r, ref_r) < 1e-6, step
-        tol = 2e-3 if dtype == torch.bfloat16 else 1e-5
-        r = rel_l2(got_x.float(), ref_x.float())
-        assert r < tol, (step, r)
-        frac = (got_x != ref_x).float().mean().item()
-        assert frac < (0.01 if dtype == torch.bfloat16 else 1.0), (step, frac)
+        if dtype == torch.bfloat16:
+            # every op of the chain rounded as torch rounds it, including the clip scale
+            # 2.5 / ‖diff‖ = bf16(bf16(1/‖diff‖)·2.5) (torch's __rtruediv__).  What remains is
+            # the order of the fp64 projection sum Σ v0·v1 over T: it can move orth across a
+            # float / bf16 rounding tie in an isolated element (measured: 1 of 768,000 at
+            # T = 6000) — allowed up to 1e-5 of the elements, every other element bit-exact
+            mism = int((got_x != ref_x).sum())
+            assert mism <= max(1, got_x.numel() // 100_000), (step, mism, rel_l2(got_x.float(), ref_x.float()))
+            assert (got_x.float() - ref_x.float()).abs().max() <= ref_x.float().abs().max() * 2 ** -7
+        else:
+            r = rel_l2(got_x.float(), ref_x.float())
+            assert r < 1e-5, (step, r)
 
 
 def test_schedule_bit_exact_on_device(gpu_device):
@@ -475,10 +482,10 @@ def test_weight_reload_matches_fresh_handle(gpu_device):
                                    (1, 2048, 2048), (16, 4096, 2048), (128, 2048, 2048), (129, 2048, 6144),
                                    (256, 12288, 2048), (200, 2048, 1088), (300, 2048, 2048)])
 def test_gemm_splitk_small_m(gpu_device, M, N, K):
-    """Small-M paths (short songs / turbo) through the production dispatch (variant -1):
-    the weight-streaming skinny kernel (M ≤ 256, K % 128 == 0: one or two 128-row chunks,
-    rows past M read as zeros, 1–8 K splits) and the 128×128 split-K path (K % 128 != 0,
-    M > 256); store, residual and SwiGLU epilogues."""
+    """Small-M paths (short songs / turbo): the production dispatch (variant -1: the
+    128×128 split-K path) with store, residual and SwiGLU epilogues, and the weight-
+    streaming skinny kernel (A/B variants 102-104: ring depth 2-4; M ≤ 256 in one or two
+    128-row chunks, rows past M read as zeros, 1–8 K splits)."""
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -496,6 +503,13 @@ def test_gemm_splitk_small_m(gpu_device, M, N, K):
                                           ff.stream_ptr()))
     torch.cuda.synchronize()
     assert rel_l2(C2.float().cpu(), (R.float() + ref.bfloat16().float()).cpu()) < 5e-3
+    if M <= 256 and K % 128 == 0:
+        for v in (102, 103, 104):
+            Ck = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
+            ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Ck), N, M, N, K, None,
+                                                  EPI_STORE, v, ff.stream_ptr()))
+            torch.cuda.synchronize()
+            assert rel_l2(Ck.float().cpu(), ref.cpu()) < 5e-3, v
     Cs = torch.empty(M, N // 2, device=gpu_device, dtype=torch.bfloat16)
     ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cs), N // 2, M, N, K, None,
                                           EPI_SWIGLU, -1, ff.stream_ptr()))
