@@ -16,6 +16,7 @@
 //   scale_shift_tables of all layers contiguous → one modulation launch
 #include <unistd.h>
 #include <map>
+#include <mutex>
 #include <cmath>
 #include <vector>
 #include <cstring>
@@ -81,6 +82,8 @@ struct acehip_dit {
     bf16_t *ts_temb = nullptr, *ts_proj = nullptr, *ts_scratch = nullptr;
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
     void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs (short songs / turbo)
+    float *sk_part = nullptr;  // stream-K partial tiles (gemm_sk_kernel) + ready flags (zeroed)
+    int *sk_flag = nullptr;
     size_t tmp_elems = 0;
 
     // optional per-kernel event timing (acehip_dit_profile)
@@ -133,6 +136,8 @@ static int forward_f32(acehip_dit *h, const float *xt, const float *ctx, int Bx,
 static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
     g.ws = h->gemm_ws;
     g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
+    g.sk_part = h->sk_part;
+    g.sk_flag = h->sk_flag;
     return gemm(g, s);
 }
 
@@ -321,6 +326,9 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
+    h->sk_part = (float *)A(SK_PART_BYTES / 2);
+    h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
+    if (h->sk_flag && hipMemset(h->sk_flag, 0, SK_MAX_BLOCKS * 4) != hipSuccess) ok = false;
     h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
     h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
     h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
@@ -888,14 +896,35 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
     return gemm(g, (hipStream_t)stream);
 }
 
-// lazily allocated split-K workspace of the standalone kernel entry points (one per device)
+// lazily allocated split-K and stream-K workspaces of the standalone kernel entry points
+// (one per device; the stream-K ready flags start zeroed and every launch leaves them zero)
+static std::mutex g_abi_ws_mu;
 static void *abi_gemm_ws() {
     static std::map<int, void *> by_dev;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_abi_ws_mu);
     void *&ws = by_dev[dev];
     if (!ws && hipMalloc(&ws, GEMM_WS_BYTES) != hipSuccess) ws = nullptr;
     return ws;
+}
+static void abi_sk_ws(GemmArgs &g) {
+    static std::map<int, std::pair<float *, int *>> by_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_abi_ws_mu);
+    auto &e = by_dev[dev];
+    if (!e.first) {
+        void *p = nullptr, *f = nullptr;
+        if (hipMalloc(&p, SK_PART_BYTES) != hipSuccess) return;
+        if (hipMalloc(&f, SK_MAX_BLOCKS * 4) != hipSuccess || hipMemset(f, 0, SK_MAX_BLOCKS * 4) != hipSuccess) {
+            (void)hipFree(p);
+            return;
+        }
+        e = {(float *)p, (int *)f};
+    }
+    g.sk_part = e.first;
+    g.sk_flag = e.second;
 }
 
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,
@@ -914,10 +943,12 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
         g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
         return gemm_small(g, variant - 100, (hipStream_t)stream);
     }
-    if (variant < 0) {   // production dispatch incl. split-K for small grids
+    if (variant < 0 || variant == 14) {   // production dispatch (split-K, stream-K) / forced stream-K
         g.ws = abi_gemm_ws();
         g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
+        abi_sk_ws(g);
         if (epi == 2) g.ldr = ldc;
+        if (variant == 14) return gemm_sk_forced(g, (hipStream_t)stream);
         return gemm(g, (hipStream_t)stream);
     }
     return gemm_variant(g, variant, (hipStream_t)stream);
@@ -949,6 +980,7 @@ int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int 
     g.hp.q = (bf16_t *)q; g.hp.k = (bf16_t *)k; g.hp.v = (bf16_t *)v; g.hp.S_dst = S; g.hp.eps = eps;
     g.ws = abi_gemm_ws();
     g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
+    abi_sk_ws(g);
     return gemm(g, (hipStream_t)stream);
 }
 

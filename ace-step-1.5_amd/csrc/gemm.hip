@@ -64,7 +64,7 @@ __device__ __forceinline__ void ring_barrier() {
 // sub-tile: one 16-B load / store per operand instead of two 8-B ones (the
 // epilogue is store-issue-bound, MI355X_MICROARCH "attention epilogue store
 // tail").  SwiGLU: the wave's columns are whole 64-column panels [32 gate | 32 up].
-template <int SM, int SN, int EPI>
+template <int SM, int SN, int EPI, int CHMAX = 12>
 __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&acc)[SM][SN], int row0, int col0,
                                               int fr, int fc) {
     static_assert(SN % 2 == 0, "sub-tiles are paired");
@@ -96,7 +96,7 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
         // before its first store: the stores may alias them (in-place residual: C == res),
         // so the compiler would otherwise wait for every load right after issuing it —
         // one full memory latency per 16-B store, exposed at one wave per SIMD
-        constexpr int NP = SN / 2, CH = (12 / NP) < 1 ? 1 : (12 / NP);
+        constexpr int NP = SN / 2, CH = (CHMAX / NP) < 1 ? 1 : (CHMAX / NP);
 #pragma unroll
         for (int c0 = 0; c0 < SM; c0 += CH) {
             uint4 rv[CH][NP], gv[CH][NP];
@@ -930,6 +930,320 @@ int launch_w4(const GemmArgs &a, hipStream_t s) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Stream-K variant of the 256×256 ping-pong tile (N ≤ 4096 projections whose grid is not a
+// whole number of rounds: down / self-O at M = 6000 are 192 tiles of 256² on 256 CUs — the
+// 192×256 tile fills one round but does 0.82× the work per cycle).  The grid is one block
+// per CU; the tiles' K-iterations, concatenated in tile order, are split into equal ranges
+// (block i: iterations [I·i/G, I·(i+1)/G)), so every CU multiplies the same number of
+// K-tiles.  A range is at most: the late part of one tile (it FINISHES that tile), whole
+// tiles, and the head (or a middle part) of one more tile (it CONTRIBUTES to it).  Each
+// block runs its contribution first — fp32 partial tile to its own workspace slot
+// (write-through sc1 stores), then a ready flag — and then its finishing segments; a
+// finisher whose tile began in earlier blocks' ranges adds their partials (in block
+// order: deterministic) before the tile's epilogue.  Flags are reset by their consumer, so
+// the next launch (or a graph replay) starts from zero.  Deadlock-free: a block waits only
+// for contributions, which every block issues before any wait, and the grid (one 128-KiB
+// block per CU, grid = CU count) is co-resident; the spin is bounded regardless.
+struct SkArgs {
+    float *part;        // [G][8 waves][32 fragments][64 lanes] f32x4 = 256 KiB per block
+    int *flag;          // [G] 1 = that block's partial is published
+    int G;              // grid size (= CUs)
+    int ktiles;         // K / 64
+};
+
+// compile-time loop: f(integral_constant<I>) for I in [I0, I1)
+template <int I0, int I1, typename F>
+__device__ __forceinline__ void sk_for(F &&f) {
+    if constexpr (I0 < I1) {
+        f(std::integral_constant<int, I0>{});
+        sk_for<I0 + 1, I1>(f);
+    }
+}
+// accumulator fragment (4 AGPRs from number A) → VGPRs
+template <int A>
+__device__ __forceinline__ f32x4 sk_acc(void) {
+    f32x4 r;
+    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+                 "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+                 : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
+                 : "n"(A), "n"(A + 1), "n"(A + 2), "n"(A + 3));
+    return r;
+}
+
+// the asm-operand captures below are required (clang rejects the implicit form) yet
+// reported as unused
+#pragma clang diagnostic ignored "-Wunused-lambda-capture"
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_sk_kernel(GemmArgs a, SkArgs sk) {
+    constexpr int BM = 256, BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
+    constexpr int ROWS = BM + BN, BUF = ROWS * 128;
+    constexpr int NA = BM / 64, NB = BN / 64;
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int fr = lane & 15, fc = lane >> 4;
+    const int arow = wr * TM, brow = BM + wc * 64;
+    const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
+    const int nk = sk.ktiles;
+    // tile t of the K-step sequence → (tm, tn) in groups of GROUP_M tile rows (as
+    // gemm_pp_kernel): the ~24 consecutive tiles of one XCD's blocks then share 8 A and
+    // 3 W panels, and all blocks start at K-tile 0 together (lockstep K-slices in L2)
+    auto tile_mn = [&](int t, int &tm, int &tn) {
+        const int per_group = GROUP_M * tilesN;
+        const int gid = t / per_group, first_m = gid * GROUP_M;
+        const int gsz = min(tilesM - first_m, GROUP_M);
+        tm = first_m + (t % per_group) % gsz;
+        tn = (t % per_group) / gsz;
+    };
+    const int64_t I = (int64_t)tilesM * (a.N / BN) * nk;
+    // logical block index: XCD-contiguous (blocks of one XCD take consecutive ranges, so a
+    // contributor and its finisher mostly share the XCD's L2)
+    const int blk = xcd_remap(blockIdx.x, sk.G);
+    auto range_start = [&](int b) { return (int64_t)b * I / sk.G; };
+    const int64_t s0 = range_start(blk), e0 = range_start(blk + 1);
+
+    // Segments in processing order: the contribution (the range ends inside tile tc: its
+    // first or a middle part), then the finished tiles from tf1 − 1 DOWN to tf0 (only tf0
+    // can start mid-tile: it needs the earlier blocks' partials, published long before).
+    // One continuous K-step sequence q = 0 .. e0 − s0 − 1 over all of them, so the LDS-DMA
+    // pipeline runs straight across segment boundaries (the next tile's first K-tiles are
+    // staged during the previous tile's last ones).
+    const int64_t tc = e0 / nk, tf0 = s0 / nk, tf1 = e0 / nk;
+    const bool contrib = e0 % nk != 0;
+    const int c_kb = contrib ? (int)(max(s0, tc * nk) - tc * nk) : 0;
+    const int c_len = contrib ? (int)(e0 - tc * nk) - c_kb : 0;
+    const int f_kb = (int)(s0 - tf0 * nk);                   // tf0's first K-tile
+    const int Q = (int)(e0 - s0);
+    // K-step cursors (tile, K-tile, segment end, segment index), advanced by one step per
+    // main-loop iteration with scalar arithmetic: cA for the A staging (step q + 1), cB for
+    // the B staging (q + 2), cM for the step being multiplied (q)
+    struct Cur { int t, k, ke, sg; };
+    auto seg_begin = [&](Cur &c) {
+        if (contrib && c.sg == 0) {
+            c.t = (int)tc; c.k = c_kb; c.ke = c_kb + c_len;
+        } else {
+            const int j = c.sg - (contrib ? 1 : 0);
+            c.t = (int)(tf1 - 1 - j);
+            c.k = (c.t == (int)tf0) ? f_kb : 0;
+            c.ke = nk;
+        }
+    };
+    auto advance = [&](Cur &c) {
+        if (++c.k == c.ke) { ++c.sg; seg_begin(c); }
+    };
+
+    auto bar = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // staging sources: per-lane panel-row pointers of the cursor's tile, rebuilt only when
+    // the staged step enters a new tile (per stage: one 64-bit add per LDS-DMA)
+    const bf16_t *srcA[NA], *srcB[NB];
+    int tA = -1, tB = -1;
+    auto set_srcA = [&](int t) {
+        int tm, tn;
+        tile_mn(t, tm, tn);
+        const int m0 = tm * BM;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int r = (wave + 8 * i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            srcA[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8;
+        }
+        tA = t;
+    };
+    auto set_srcB = [&](int t) {
+        int tm, tn;
+        tile_mn(t, tm, tn);
+        const int n0 = tn * BN;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const int r = (wave + 8 * i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (((BM + r) >> 1) & 7);
+            srcB[i] = a.W + (int64_t)(n0 + r) * a.ldw + c * 8;
+        }
+        tB = t;
+    };
+    auto stageA = [&](int buf, const Cur &c) {
+        if (c.t != tA) set_srcA(c.t);
+        char *b = lds + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) glds16(srcA[i] + c.k * BK, b + (wave + 8 * i) * 1024);
+    };
+    auto stageB = [&](int buf, const Cur &c) {
+        if (c.t != tB) set_srcB(c.t);
+        char *b = lds + buf * BUF + BM * 128;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) glds16(srcB[i] + c.k * BK, b + (wave + 8 * i) * 1024);
+    };
+    auto lane_l = [&] { int v = lane; asm volatile("" : "+v"(v)); return v; };
+    // The accumulators live in a[0:127] BY NUMBER (fragment (i, j) at a[16i + 4j]) and are
+    // touched only by inline asm: MFMAs, the zeroing writes and the reads of the segment
+    // finish.  hipcc, left with ≤ 128 VGPRs and no MFMA of its own, allocates no AGPR (the
+    // a127 clobber makes the kernel descriptor reserve them) — with accumulators as C++
+    // values it shuffled them between VGPRs, AGPRs and scratch around the finish code.
+    auto acc_zero = [] {
+        sk_for<0, 128>([&](auto R) __attribute__((always_inline)) {
+            asm volatile("v_accvgpr_write_b32 a%c0, 0" ::"n"(decltype(R)::value));
+        });
+        asm volatile("s_nop 2" ::: "a0", "a127");   // v_accvgpr_write → MFMA srcC read
+    };
+    acc_zero();
+    bf16x8 xk[SMH], bk[4];
+    auto readA1 = [&](const char *b, int h, int ks) {
+#pragma unroll
+        for (int i = 0; i < SMH; ++i) xk[i] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
+    };
+    auto readB1 = [&](const char *b, int ks) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bk[j] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
+    };
+    // MFMAs by inline asm with the accumulators tied to AGPRs ("+a"): the segment finish
+    // (epilogue / partial store / partial add) then draws on the VGPRs alone — with the
+    // builtin, hipcc kept them in VGPRs and spilled ~160 registers around the finish code
+    auto mma1 = [&](auto HC) __attribute__((always_inline)) {
+        constexpr int h = decltype(HC)::value;
+        bf16x8 *bkp = bk, *xkp = xk;
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        sk_for<0, SMH * 4>([bkp, xkp](auto G) __attribute__((always_inline)) {
+            constexpr int g = decltype(G)::value, i = g / 4, j = g % 4, A = ((h * SMH + i) * 4 + j) * 4;
+            asm volatile("v_mfma_f32_16x16x32_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                         ::"n"(A), "n"(A + 3), "v"(bkp[j]), "v"(xkp[i]));
+        });
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // this block's partial slot: fragment f of wave w at lane l = part + ((w·32 + f)·64 + l)·4
+    auto slot = [&](int b) { return sk.part + ((int64_t)b * 512 * 32 + (int64_t)(wave * 32) * 64 + lane) * 4; };
+
+    // prologue (as gemm_pp_kernel): step 0 complete, B(1) in flight
+    Cur cM{0, 0, 0, 0}, cA{0, 0, 0, 0}, cB{0, 0, 0, 0};
+    seg_begin(cM);
+    cA = cM;
+    cB = cM;
+    if (Q > 0) {
+        stageB(0, cB);
+        stageA(0, cA);
+        advance(cA);
+        advance(cB);
+        if (Q > 1) {
+            stageB(1, cB);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        advance(cB);
+    }
+    bar();
+    if (wr == 1) bar();   // group 1 runs one barrier behind
+    for (int q = 0; q < Q; ++q) {
+        const char *b = lds + (q & 1) * BUF;
+        readB1(b, 0);
+        readA1(b, 0, 0);
+        if (q + 1 < Q) {
+            stageA((q + 1) & 1, cA);
+            advance(cA);
+        }
+        lgkm0();
+        bar();
+        mma1(std::integral_constant<int, 0>{});
+        bar();
+        readA1(b, 1, 0);
+        lgkm0();
+        bar();
+        mma1(std::integral_constant<int, 1>{});
+        bar();
+        readB1(b, 1);
+        readA1(b, 0, 1);
+        lgkm0();
+        bar();
+        mma1(std::integral_constant<int, 0>{});
+        bar();
+        readA1(b, 1, 1);
+        if (q + 2 < Q) {
+            stageB(q & 1, cB);
+            advance(cB);
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        bar();
+        mma1(std::integral_constant<int, 1>{});
+        bar();
+        const Cur st = cM;
+        advance(cM);
+        if (st.k + 1 != st.ke) continue;
+        // ---- segment end: both wave groups in step, then the tile's contribution or finish
+        if (wr == 0) bar();
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");   // XDL → VALU / store reads of acc
+        if (contrib && st.sg == 0) {
+            // fp32 partial → this block's slot (write-through), every storing wave drained,
+            // then one lane publishes the flag
+            float *p = slot(blk);
+            // one base pointer per row group (4 fragments, 4 KiB), immediate offsets within
+            // (explicit capture: hipcc does not see an implicit capture used only in asm operands)
+            sk_for<0, SM>([p](auto IC) __attribute__((always_inline)) {
+                constexpr int i = decltype(IC)::value;
+                const f32x4 v0 = sk_acc<16 * i>(), v1 = sk_acc<16 * i + 4>(), v2 = sk_acc<16 * i + 8>(),
+                            v3 = sk_acc<16 * i + 12>();
+                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\t"
+                             "global_store_dwordx4 %0, %2, off offset:1024 sc1\n\t"
+                             "global_store_dwordx4 %0, %3, off offset:2048 sc1\n\t"
+                             "global_store_dwordx4 %0, %4, off offset:3072 sc1"
+                             ::"v"(p + i * 4 * 64 * 4), "v"(v0), "v"(v1), "v"(v2), "v"(v3) : "memory");
+            });
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(sk.flag + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const int64_t t = st.t;
+            const bool fix = t == tf0 && f_kb > 0;
+            if (fix) {
+                // the tile's first f_kb K-tiles are block blk − 1's contribution (the host
+                // admits only splits with one contributor per tile, sk_split_ok)
+                if (tid == 0) {
+                    int spins = 0;
+                    while (__hip_atomic_load(sk.flag + blk - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1 &&
+                           ++spins < (1 << 22))
+                        __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+            }
+            // epilogue one row group at a time (the fragments read out of the AGPRs, the
+            // contributor's partial added first)
+            int tm, tn;
+            tile_mn((int)t, tm, tn);
+            const int row0 = tm * BM + arow, col0 = tn * BN + wc * 64;
+            const int ln = lane_l(), frl = ln & 15, fcl = ln >> 4;
+            const float *pp = sk.part + ((int64_t)(blk - 1) * 512 * 32 + (int64_t)(wave * 32) * 64 + ln) * 4;
+            sk_for<0, SM>([&](auto IC) __attribute__((always_inline)) {
+                constexpr int i = decltype(IC)::value;
+                f32x4 c[1][4] = {{sk_acc<16 * i>(), sk_acc<16 * i + 4>(), sk_acc<16 * i + 8>(), sk_acc<16 * i + 12>()}};
+                if (fix) {
+                    const float *pi = pp + i * 4 * 64 * 4;
+                    asm volatile("" : "+v"(pi));   // rebuilt here, not hoisted out of the main loop
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) c[0][j] += *(const f32x4 *)(pi + j * 64 * 4);
+                }
+                epilogue_tile<1, 4, EPI, 2>(a, c, row0 + 16 * i, col0, frl, fcl);
+            });
+            if (fix) {
+                __syncthreads();   // every wave read the partial before the slot is released
+                if (tid == 0) __hip_atomic_store(sk.flag + blk - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        acc_zero();
+        if (wr == 1) bar();   // group 1 one barrier behind again
+    }
+    if (wr == 0) bar();   // balance the barrier count
+}
+
 template <int BM>
 int launch_pp(const GemmArgs &a, hipStream_t s) {
     if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
@@ -1177,6 +1491,71 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     return gemm_variant(tl, tv, s);
 }
 
+// Stream-K dispatch of the 256×256 ping-pong tile (gemm_sk_kernel): needs the handle's
+// stream-K workspace (a.sk_part / a.sk_flag) and N % 256 == 0, epilogues that work on one
+// finished tile in registers (store, residual, gated residual, SwiGLU).
+// ACEHIP_GEMM_SK: 0 off (default), 1 on where the cost model prefers it, 2 forced (A/B).
+// Measured (cold weights, µs, tools/bench_gemm.py; v11 = the 192/256 tail-split path):
+//   eq_k6144 8192×2048×6144 (256 tiles, no hand-off)  v7 149.4  v14 156.6
+//   down  v11 130.7  v14 138.6     qkv  v11 94.8  v14 98.9     o  v11 47.5  v14 59.6
+//   swiglu  v11 287.4  v14 302.1 (290.6 vs 300.3 on another box)
+// i.e. ~5 % main-loop cost for the cursor bookkeeping + ~20 µs of partial hand-off on
+// down (256 KB fp32 per contributor written, then re-read by a latency-bound
+// chunked epilogue) — it loses everywhere, so it stays an A/B variant (14).
+static int sk_mode() {   // read per call: in-process A/B (tools/ab_env_song.py)
+    const char *e = getenv("ACEHIP_GEMM_SK");
+    return e ? atoi(e) : 0;
+}
+// every tile split between at most two blocks (one contributor: the kernel's fixup reads
+// block blk − 1 only) and no block range strictly inside one tile
+static bool sk_split_ok(int64_t tiles, int nk, int G) {
+    const int64_t I = tiles * nk;
+    for (int b = 0; b < G; ++b) {
+        const int64_t s0 = (int64_t)b * I / G, e0 = (int64_t)(b + 1) * I / G;
+        if (e0 <= s0) return false;
+        if (s0 % nk && s0 / nk == (e0 - 1) / nk && e0 % nk) return false;     // middle part
+        if (s0 % nk && b > 0 && (int64_t)(b - 1) * I / G > (s0 / nk) * nk) return false;   // 2+ contributors
+    }
+    return true;
+}
+static int gemm_sk(const GemmArgs &a, hipStream_t s) {
+    SkArgs sk{};
+    sk.part = a.sk_part;
+    sk.flag = a.sk_flag;
+    sk.G = std::min(num_cus(), SK_MAX_BLOCKS);
+    sk.ktiles = a.K / BK;
+    if (!sk_split_ok((int64_t)((a.M + 255) / 256) * (a.N / 256), sk.ktiles, sk.G))
+        return fail(-1, "gemm_sk: split with more than one contributor per tile");
+    switch (a.epi) {
+        case EPI_STORE: gemm_sk_kernel<EPI_STORE><<<sk.G, 512, 0, s>>>(a, sk); break;
+        case EPI_GATED_RES: gemm_sk_kernel<EPI_GATED_RES><<<sk.G, 512, 0, s>>>(a, sk); break;
+        case EPI_RES: gemm_sk_kernel<EPI_RES><<<sk.G, 512, 0, s>>>(a, sk); break;
+        case EPI_SWIGLU: gemm_sk_kernel<EPI_SWIGLU><<<sk.G, 512, 0, s>>>(a, sk); break;
+        default: return fail(-1, "gemm_sk: epilogue");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+int gemm_sk_forced(const GemmArgs &a, hipStream_t s) {
+    if (!a.sk_part || !a.sk_flag || a.N % 256 || a.K % BK || a.K < 4 * BK) return fail(-1, "gemm_sk: shape / workspace");
+    return gemm_sk(a, s);
+}
+// stream-K time in 192×256-tile rounds (cost model of gemm_pick_variant: a 256² tile =
+// 1.093 of a 192×256 one) + the partial hand-off, vs the chosen variant's rounds
+static bool prefer_sk(const GemmArgs &a, int v) {
+    const int m = sk_mode();
+    if (m == 0 || !a.sk_part || !a.sk_flag || a.N % 256 || a.K < 4 * BK) return false;
+    if (a.epi != EPI_STORE && a.epi != EPI_GATED_RES && a.epi != EPI_RES && a.epi != EPI_SWIGLU) return false;
+    const int cus = num_cus();
+    if (!sk_split_ok((int64_t)((a.M + 255) / 256) * (a.N / 256), a.K / BK, std::min(cus, SK_MAX_BLOCKS))) return false;
+    if (m == 2) return true;
+    const int64_t t7 = ((a.M + 255) / 256) * (a.N / 256), t8 = ((a.M + 191) / 192) * (a.N / 256);
+    if (t7 < cus / 2) return false;
+    const double sk = (double)t7 * 1.093 / cus + 0.06;
+    const double cur = v == 7 ? (double)((t7 + cus - 1) / cus) * 1.093 : (double)((t8 + cus - 1) / cus);
+    return sk < cur * 0.97;
+}
+
 // small-M A/B entry (tools/bench_skinny.py): mode 2..4 = the skinny kernel at that ring
 // depth, 0 = the 128×128 split-K path; needs a.ws
 int gemm_small(const GemmArgs &a, int mode, hipStream_t s) {
@@ -1251,6 +1630,7 @@ int gemm(const GemmArgs &a, hipStream_t s) {
     int v = g_variant_override;
     if (v < 0) {
         v = gemm_pick_variant(a.M, a.N);
+        if ((v == 7 || v == 8 || v == 11) && prefer_sk(a, v)) return gemm_sk(a, s);
         if (v == 7 || v == 8 || v == 11) {
             const int rc = gemm_tail_split(a, v, s);
             if (rc <= 0) return rc;   // split done (0) or failed (< 0); 1 = not applicable

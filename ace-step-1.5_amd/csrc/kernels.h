@@ -39,13 +39,19 @@ struct GemmArgs {
     // split-K workspace (grids too small to fill the chip): fp32 partials [splits][M][N]
     // + a bf16 [M][N] staging tile for the head-post case; null disables split-K
     void *ws; size_t ws_bytes;
+    // stream-K workspace (gemm_sk_kernel): SK_MAX_BLOCKS partial tiles of 256 KiB + as many
+    // ready flags (zeroed at allocation; every launch leaves them zero); null disables
+    float *sk_part; int *sk_flag;
     int kper;                       // internal: K-tiles per split (EPI_PARTIAL launches)
 };
 constexpr int EPI_PARTIAL = 5;
+constexpr int SK_MAX_BLOCKS = 256;
+constexpr size_t SK_PART_BYTES = (size_t)SK_MAX_BLOCKS << 18;   // 256 KiB per block
 constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace      // internal: store the fp32 accumulators of split blockIdx.y to ws
 int gemm(const GemmArgs &a, hipStream_t s);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
 int gemm_small(const GemmArgs &a, int mode, hipStream_t s);        // small-M A/B (needs ws)
+int gemm_sk_forced(const GemmArgs &a, hipStream_t s);              // stream-K 256² tile (needs sk_*)
 
 // --------------------------------------------------------------- small ops --
 // y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16

@@ -346,7 +346,8 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
  * need N % 256 == 0; -1: the production choice, including the weight-streaming
  * kernel for M <= 256 and split-K for grids that cannot fill half the chip;
  * 100 + d: the weight-streaming kernel with a d-deep register ring (d = 2..4),
- * 100: the 128x128 split-K path — small-M A/B) — tuning and tests. */
+ * 100: the 128x128 split-K path — small-M A/B; 14: the stream-K 256x256 ping-pong
+ * tile, N % 256 == 0) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 

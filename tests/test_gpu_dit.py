@@ -519,6 +519,54 @@ def test_gemm_splitk_small_m(gpu_device, M, N, K):
     assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(6000, 2048, 6144), (6000, 2048, 2048), (6000, 4096, 2048), (6000, 12288, 2048),
+                                   (15000, 2048, 6144), (1000, 512, 1024), (700, 768, 512)])
+def test_gemm_streamk(gpu_device, M, N, K):
+    """Stream-K 256×256 ping-pong tile (variant 14): every CU multiplies the same number of
+    K-tiles, tiles split between two CUs are finished by adding the contributor's fp32
+    partial (flag hand-off).  Store, residual and SwiGLU epilogues vs fp32 torch; twice in a
+    row (the ready flags must be left at zero for the next launch); the production dispatch
+    (-1) agrees.  Shapes whose split would need two contributors per tile are refused."""
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(gpu_device, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(gpu_device, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    C = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
+    rc = ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, ff.ptr(b), EPI_STORE, 14,
+                                      ff.stream_ptr())
+    if rc != 0:
+        assert b"contributor" in ff.lib().acehip_last_error()
+        pytest.skip("split needs two contributors per tile: refused")
+    torch.cuda.synchronize()
+    assert rel_l2(C.float().cpu(), (ref + b.float()).cpu()) < 5e-3
+    C1 = C.clone()
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, ff.ptr(b), EPI_STORE, 14,
+                                          ff.stream_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(C, C1)                                    # deterministic, flags reset
+    R = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
+    C2 = R.clone()
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C2), N, M, N, K, None, EPI_RES, 14,
+                                          ff.stream_ptr()))
+    torch.cuda.synchronize()
+    assert rel_l2(C2.float().cpu(), (R.float() + ref.bfloat16().float()).cpu()) < 5e-3
+    if N % 64 == 0 and N >= 512:
+        Cs = torch.empty(M, N // 2, device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cs), N // 2, M, N, K, None,
+                                              EPI_SWIGLU, 14, ff.stream_ptr()))
+        torch.cuda.synchronize()
+        y = ref.bfloat16().float().view(M, N // 64, 2, 32)
+        gate, up = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
+        assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2
+    Cp = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cp), N, M, N, K, ff.ptr(b), EPI_STORE,
+                                          -1, ff.stream_ptr()))
+    torch.cuda.synchronize()
+    assert rel_l2(Cp.float().cpu(), C.float().cpu()) < 5e-3
+
+
 def test_forward_graph_replay_matches_eager(gpu_device):
     """acehip_dit_set_graph: the captured layer-stack graph gives bit-identical outputs to
     eager launches across new t / xt / out pointers, a new condition of the same shape,
