@@ -507,7 +507,20 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
 // RAW: each wave's vmcnt precedes the barrier that opens the first read of
 // the tile (barrier 8kt+8 for group 0).  Two LDS tile buffers, ~1 tile of
 // DMA lead for A and ~1.25 for B.
-template <int BM, int EPI>
+// DBG (diagnostic variants 20-22 only, results meaningless): bit 0 drops the main-loop
+// LDS-DMA, bit 1 the main-loop fragment reads (SCHED 1).
+// SPL (SCHED 1 only): how the LDS-DMA pieces of a K-tile are spread over its phases —
+//   0  A(kt+1) all in phase 0, B(kt+2) all in phase 3
+//   1  A(kt+1) half in phase 0, half in phase 1; B(kt+2) all in phase 3
+//   2  A(kt+1) half in phase 0, half in phase 1; B(kt+2) first half in phase 3, second
+//      half in the next K-tile's phase 0 (as B(kt+1))
+//   3  as 2, but B(kt+1)'s second half in phase 1 (phase 0 carries only its 8 reads + 2);
+//      the 256-row default: interleaved 5-round medians (tools/bench_gemm.py ROUNDS=5, cold
+//      weights) SwiGLU 251.3 vs 257.3 µs, QKV 91.7 vs 95.0, down 128.6 vs 133.4 against 0
+//      (the ablation behind it: without the main-loop DMA the 256² tile ran 22 % faster,
+//      without the fragment reads 18 %, without both 37 %)
+// SCHED 0 takes SPL 1 only: A(kt+1) split between phases 0 and 1 (phase 3 has no reads)
+template <int BM, int EPI, int DBG = 0, int SPL = (BM == 256 ? 3 : 0), int SCH = -1>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
     constexpr int ROWS = BM + BN, BUF = ROWS * 128;
@@ -550,6 +563,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) glds16(srcB[i] + k0, b + (wave + 8 * i) * 1024);
     };
+    auto stageAp = [&](int buf, int k0, int i0, int i1) {
+        char *b = lds + buf * BUF;
+#pragma unroll
+        for (int i = i0; i < i1; ++i) glds16(srcA[i] + k0, b + (wave + 8 * i) * 1024);
+    };
+    auto stageBp = [&](int buf, int k0, int i0, int i1) {
+        char *b = lds + buf * BUF + BM * 128;
+#pragma unroll
+        for (int i = i0; i < i1; ++i) glds16(srcB[i] + k0, b + (wave + 8 * i) * 1024);
+    };
     auto bar = [] {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -569,7 +592,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     // prologue: tile 0 complete, B(1) in flight
     stageB(0, 0);
     stageA(0, 0);
-    if (nk > 1) {
+    if (SPL >= 2 && nk > 1) {
+        stageBp(1, BK, 0, NB / 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB / 2) : "memory");
+    } else if (nk > 1) {
         stageB(1, BK);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
     } else {
@@ -578,7 +604,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     bar();
     if (wr == 1) bar();   // group 1 runs one barrier behind
 
-    constexpr int SCHED = PP_SCHED >= 0 ? PP_SCHED : (BM == 256 ? 1 : 0);
+    constexpr int SCHED = SCH >= 0 ? SCH : PP_SCHED >= 0 ? PP_SCHED : (BM == 256 ? 1 : 0);
+    static_assert(SPL == 0 || SCHED == 1 || (SCHED == 0 && SPL == 1), "LDS-DMA spread: SCHED 1, or SPL 1 on SCHED 0");
     if constexpr (SCHED == 2) {
     // Two phases per K-tile (k-step 0, k-step 1; 32 MFMAs each): half the barriers of
     // the 4-phase schedules.  Phase 0 stages the whole next tile (A and B) into the
@@ -632,10 +659,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     // after tile kt's phase-2 reads) are one barrier each.
     bf16x8 xk[SMH], bk[4];
     auto readA1 = [&](const char *b, int h, int ks) {
+        if constexpr (DBG & 2) return;
 #pragma unroll
         for (int i = 0; i < SMH; ++i) xk[i] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
     };
     auto readB1 = [&](const char *b, int ks) {
+        if constexpr (DBG & 2) return;
 #pragma unroll
         for (int j = 0; j < 4; ++j) bk[j] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
     };
@@ -654,12 +683,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         const char *b = lds + (kt & 1) * BUF;
         readB1(b, 0);
         readA1(b, 0, 0);
-        if (kt + 1 < nk) stageA((kt + 1) & 1, (kt + 1) * BK);
+        if (!(DBG & 1) && kt + 1 < nk) {
+            if constexpr (SPL == 0) stageA((kt + 1) & 1, (kt + 1) * BK);
+            else stageAp((kt + 1) & 1, (kt + 1) * BK, 0, NA / 2);
+            if constexpr (SPL == 2) stageBp((kt + 1) & 1, (kt + 1) * BK, NB / 2, NB);
+        }
         lgkm0();
         bar();
         mma1(0);
         bar();
         readA1(b, 1, 0);
+        if (SPL != 0 && !(DBG & 1) && kt + 1 < nk) {
+            stageAp((kt + 1) & 1, (kt + 1) * BK, NA / 2, NA);
+            if constexpr (SPL == 3) stageBp((kt + 1) & 1, (kt + 1) * BK, NB / 2, NB);
+        }
         lgkm0();
         bar();
         mma1(1);
@@ -671,7 +708,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         mma1(0);
         bar();
         readA1(b, 1, 1);
-        if (kt + 2 < nk) {
+        if (SPL >= 2 && !(DBG & 1) && kt + 2 < nk) {
+            stageBp(kt & 1, (kt + 2) * BK, 0, NB / 2);
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB / 2) : "memory");
+        } else if (!(DBG & 1) && kt + 2 < nk) {
             stageB(kt & 1, (kt + 2) * BK);
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB) : "memory");
         } else {
@@ -716,12 +756,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         // phase 0
         readB(b, 0, b0);
         readA(b, 0);
-        if (kt + 1 < nk) stageA((kt + 1) & 1, (kt + 1) * BK);
+        if (kt + 1 < nk) {
+            if constexpr (SPL == 1) stageAp((kt + 1) & 1, (kt + 1) * BK, 0, NA / 2);
+            else stageA((kt + 1) & 1, (kt + 1) * BK);
+        }
         bar();
         mma(0, 0, b0);
         bar();
         // phase 1
         readB(b, 1, b1);
+        if (SPL == 1 && kt + 1 < nk) stageAp((kt + 1) & 1, (kt + 1) * BK, NA / 2, NA);
         bar();
         mma(0, 1, b1);
         bar();
@@ -772,7 +816,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 //            ∥ ds_reads of tile kt+1's k-step 0 → F0
 // so the MFMA pipe never waits for a fragment read, the DMA of a tile has one whole
 // K-tile (≈96 MFMAs) of lead, and two LDS buffers suffice.
-template <int BM, int BN, int EPI>
+// DBG 1: no main-loop refill (diagnostic 29).
+// VG 1: the main-loop refill goes through VGPRs instead of LDS-DMA — each wave holds the
+// next refill's PW pieces in registers (buffer_load_dwordx4, issued one K-tile ahead) and
+// writes them with ds_write_b128 at the hook points where the DMA pieces were issued (the
+// prologue still stages tiles 0..NS−1 by LDS-DMA).  An LDS-DMA piece costs its wave ≈60
+// cycles of issue among MFMAs (MI355X_MICROARCH.md, per-instruction constants); the plain
+// load + store pair is meant to cost less.
+template <int BM, int BN, int EPI, int DBG = 0, int VG = 0>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     constexpr int TM = BM / 2, TN = BN / 2, SM = TM / 16, SN = TN / 16;
     constexpr int ROWS = BM + BN, STAGE = ROWS * 128;
@@ -805,6 +856,28 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
         else src[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8;
     }
     auto stage1 = [&](int buf, int k0, int i) { glds16(src[i] + k0, lds + buf * STAGE + (wave + 4 * i) * 1024); };
+    // VG: buffer resources over this tile's A rows (rows past M read as zeros) and W rows;
+    // piece i is 32 image rows below piece i−1, its source column chunk is the same
+    // (the swizzle term (r >> 1) & 7 does not change over 32 rows)
+    constexpr int PA = BM / 32;                                   // pieces of A rows
+    static_assert(BM % 32 == 0, "A pieces must be whole");
+    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.A + (int64_t)m0 * a.lda), 0, (int)min((int64_t)(a.M - m0) * a.lda * 2, (int64_t)0x7fffffff),
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t rsW =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(a.W + (int64_t)n0 * a.ldw), 0, BN * a.ldw * 2, 0x00020000);
+    const int vr0 = wave * 8 + (lane >> 3), vc = (lane & 7) ^ ((vr0 >> 1) & 7);
+    const int voA = (vr0 * a.lda + vc * 8) * 2, voW = (vr0 * a.ldw + vc * 8) * 2;
+    u32x4 stg[VG ? PW : 1];
+    auto vload = [&](int k0, int i) {
+        if constexpr (VG) {
+            if (i < PA) stg[i] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voA + i * 64 * a.lda, k0 * 2, 0);
+            else stg[i] = __builtin_amdgcn_raw_buffer_load_b128(rsW, voW + (i - PA) * 64 * a.ldw, k0 * 2, 0);
+        }
+    };
+    auto vstore = [&](int buf, int i) {
+        if constexpr (VG) *(u32x4 *)(lds + buf * STAGE + (wave + 4 * i) * 1024 + lane * 16) = stg[i];
+    };
 
     f32x4 acc[SM][SN];
 #pragma unroll
@@ -840,7 +913,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     // the wait is the builtin (vmcnt((NS−2)·PW) expcnt(7) lgkmcnt(0): tile kt+1 landed,
     // the NS−2 newer refills still in flight), so the compiler's own waitcnt pass knows
     // every read before it has retired and adds none after it
-    constexpr int VM = (NS - 2) * PW;
+    // (VG: the PW register loads of the next refill stay in flight across the barrier; the
+    // prologue's LDS-DMA of tile kt+1 is older than them)
+    constexpr int VM = VG ? PW : (NS - 2) * PW;
     static_assert(VM < 64, "vmcnt field");
     constexpr int WAIT_ENC = 0x0070 | (VM & 15) | ((VM >> 4) << 14);
     auto bar = [] {
@@ -865,7 +940,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     for (int t = 0; t < NS; ++t)
 #pragma unroll
         for (int i = 0; i < PW; ++i) stage1(t, min(t, nk - 1) * BK, i);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
+    if constexpr (VG) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) vload(min(NS, nk - 1) * BK, i);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS * PW) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd(lds, 0, x0, w0);
@@ -880,14 +961,30 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
         bar();
         // refill of this tile's buffer (every wave is past its reads) with tile kt+NS
         const int kr = min(kt + NS, nk - 1) * BK;
+        const int kr1 = min(kt + NS + 1, nk - 1) * BK;   // VG: the refill after this one
         if constexpr (FIRST < 0) {
 #pragma unroll
-            for (int i = 0; i < PW; ++i) stage1(cur, kr, i);
+            for (int i = 0; i < PW; ++i) {
+                if constexpr (VG) {
+                    vstore(cur, i);
+                    vload(kr1, i);
+                } else {
+                    stage1(cur, kr, i);
+                }
+            }
         }
         rd(lds + nxt * STAGE, 0, x0, w0);
         mm(x1, w1, [&](int n) {
-            if (FIRST >= 0 && n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW)
-                stage1(cur, kr, (n - FIRST) / EVERY);
+            if (!(DBG & 1) && FIRST >= 0 && n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW) {
+                if constexpr (VG) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    vstore(cur, (n - FIRST) / EVERY);
+                    vload(kr1, (n - FIRST) / EVERY);
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    stage1(cur, kr, (n - FIRST) / EVERY);
+                }
+            }
         });
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1299,6 +1396,24 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 11: return launch_w4<192>(a, s);             // 4 waves, 96x128 wave tile, pipelined fragments
         case 12: return launch_pp<128>(a, s);             // ping-pong 128x256 (96 KiB), 64x64 wave tiles
         case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
+        case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30: {
+            // diagnostics / A/B: pp store, see gemm_pp_kernel DBG and SPL
+            if (a.N % 256 || a.epi != EPI_STORE) return fail(-1, "gemm: diagnostic variant");
+            const int tiles = ((a.M + 255) / 256) * (a.N / 256), t192 = ((a.M + 191) / 192) * (a.N / 256);
+            if (variant == 20) gemm_pp_kernel<256, EPI_STORE, 1><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 21) gemm_pp_kernel<256, EPI_STORE, 2><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 22) gemm_pp_kernel<256, EPI_STORE, 3><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 23) gemm_pp_kernel<256, EPI_STORE, 0, 0><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 24) gemm_pp_kernel<256, EPI_STORE, 0, 2><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 25) gemm_pp_kernel<192, EPI_STORE, 0, 1><<<t192, 512, 0, s>>>(a);
+            else if (variant == 27) gemm_pp_kernel<256, EPI_STORE, 0, 3><<<tiles, 512, 0, s>>>(a);
+            else if (variant == 29) gemm_w4_kernel<192, 256, EPI_STORE, 1><<<t192, 256, 0, s>>>(a);
+            else if (variant == 30) gemm_w4_kernel<192, 256, EPI_STORE, 0, 1><<<t192, 256, 0, s>>>(a);
+            else if (variant == 28) gemm_pp_kernel<192, EPI_STORE, 0, 3, 1><<<t192, 512, 0, s>>>(a);
+            else gemm_pp_kernel<192, EPI_STORE, 0, 2, 1><<<t192, 512, 0, s>>>(a);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
         default: return fail(-1, "gemm: bad variant");
     }
 }

@@ -28,7 +28,11 @@ for name, (M, N, K) in shapes.items():
     rot = [0]
     fl = 2.0 * M * N * K
     row = {}
-    for v in variants:
+    times = {}
+    # ROUNDS > 1: the variants are timed in interleaved rounds (v1 v2 … v1 v2 …) and the
+    # median per variant is reported, so clock drift over the run does not favour one
+    for rd in range(int(os.environ.get("ROUNDS", "1"))):
+      for v in variants:
         if v in (3, 5, 6, 7, 8, 9, 10, 11, 12, 14) and N % 256:
             continue
         def run():
@@ -45,7 +49,8 @@ for name, (M, N, K) in shapes.items():
         e0.record()
         for _ in range(n): run()
         e1.record(); torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / n * 1e3
+        times.setdefault(v, []).append(e0.elapsed_time(e1) / n * 1e3)
+        us = sorted(times[v])[len(times[v]) // 2]
         row[f"v{v}"] = {"us": round(us, 1), "tflops": round(fl / us * 1e-6, 1), "rel": round(err, 5)}
     Wts = [w.t() for w in Ws]
     for i in range(3): torch.matmul(A, Wts[i % nrot])
