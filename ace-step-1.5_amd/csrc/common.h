@@ -80,6 +80,33 @@ __device__ __forceinline__ void pair8(const f32x4 &lo, const f32x4 &hi, bool odd
 }
 
 // ------------------------------------------------------- wave reductions ---
+// Σ_{sp < splits} p[sp·plane + 0..7] summed in split order (the split-K epilogue's own
+// order, so a consumer that folds it in rounds identically); four splits' loads in flight at
+// a time from clamped indices, the extra ones dropped by a select (no branch around a load)
+__device__ __forceinline__ void sum_parts8(const float *p, int64_t plane, int splits, float (&acc)[8]) {
+    f32x4 a0 = *(const f32x4 *)p, a1 = *(const f32x4 *)(p + 4);
+    for (int s0 = 1; s0 < splits; s0 += 4) {
+        f32x4 v0[4], v1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float *q = p + (int64_t)min(s0 + i, splits - 1) * plane;
+            v0[i] = *(const f32x4 *)q;
+            v1[i] = *(const f32x4 *)(q + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = s0 + i < splits;
+            a0 = ok ? a0 + v0[i] : a0;
+            a1 = ok ? a1 + v1[i] : a1;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        acc[c] = a0[c];
+        acc[4 + c] = a1[c];
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -133,12 +133,12 @@ static int forward_f32(acehip_dit *h, const float *xt, const float *ctx, int Bx,
                        int t_stride, int Bc, int T, float *vt_out, hipStream_t s);
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
-static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s) {
+static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s, RowAdd *defer = nullptr) {
     g.ws = h->gemm_ws;
     g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
     g.sk_part = h->sk_part;
     g.sk_flag = h->sk_flag;
-    return gemm(g, s);
+    return gemm(g, s, defer);
 }
 
 namespace {
@@ -521,7 +521,7 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
 int acehip_dit_set_uniform_rows(acehip_dit *h, int first_row, void *stream) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
     if (!h->have_cond) return fail(ACEHIP_E_STATE, "set_uniform_rows before set_condition");
-    if (first_row <= 0 || first_row > h->cond_Bc) return fail(ACEHIP_E_ARG, "set_uniform_rows: first_row in [1, Bc]");
+    if (first_row < 0 || first_row > h->cond_Bc) return fail(ACEHIP_E_ARG, "set_uniform_rows: first_row in [0, Bc]");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     h->uniform_from = 1 << 30;
@@ -739,13 +739,19 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     const bool fuse_rowadd = !(fe && fe[0] == '0');
     const size_t cper = (size_t)Bc * kvd * Le;
     const int Bq = std::min(h->uniform_from, Bc), Mq = Bq * S;   // rows with a real cross-attention
+    // small-M grids take gemm's split-K path; the residual epilogue of such a GEMM (O, cross-O,
+    // down) is then deferred into the next norm, which reads the rows anyway: `pend` carries
+    // it (gemm sets pend.part only when it deferred).  Deferral needs that norm to cover every
+    // row the GEMM wrote, and no X copy in between (the layer-0 CFG dedup).
+    RowAdd pend{};
     for (int l = 0; l < L; ++l) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
         const int64_t mbs = 6 * D;
         // --- self-attention with AdaLN-Zero (base:499-511); layer 0 of identical CFG rows: row 0
         const int Bs = (dup && l == 0) ? 1 : Bc, Ms = Bs * S;
-        RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, Ms, D, eps, s));
+        RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, Ms, D, eps, s, pend));
+        pend = RowAdd{};
         // QKV projection with q/k RMSNorm + RoPE + head-major scatter fused in the epilogue
         GemmArgs q{};
         q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D;
@@ -762,32 +768,42 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = Ms; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
-        RUN(timed(h, 3, s, [&] { return hgemm(h, o, s); }));
+        const bool defer_o = fuse_rowadd && Bs == Bc && (Mq == M || Mq == 0);
+        RUN(timed(h, 3, s, [&] { return hgemm(h, o, s, defer_o ? &pend : nullptr); }));
         for (int b = Bs; b < Bc; ++b)
             HIP_TRY(hipMemcpyAsync(h->X + (size_t)b * S * D, h->X, (size_t)S * D * 2, hipMemcpyDeviceToDevice, s));
         // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
         // rows, base:1907) get their constant cross-O output cnull[l] (set_uniform_rows)
-        RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, Mq, D, eps, s));
-        GemmArgs cq{};
-        cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D;
-        cq.M = Mq; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
-        cq.hp.B = Bq; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
-        cq.hp.eps = eps;
-        RUN(hgemm(h, cq, s));
-        RUN(timed(h, 6, s, [&] {
-            return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bq, H, KV, S, Le, -1, scale, qd,
-                             h->attn_ws, s);
-        }));
-        GemmArgs co{};
-        co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
-        co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
-        RUN(timed(h, 3, s, [&] { return hgemm(h, co, s); }));
+        if (Mq > 0) {
+            RUN(rmsnorm_mod(h->X, ly.n_ca, nullptr, nullptr, 0, S, h->XN, Mq, D, eps, s, pend));
+            pend = RowAdd{};
+            GemmArgs cq{};
+            cq.A = h->XN; cq.lda = D; cq.W = ly.wcq; cq.ldw = D;
+            cq.M = Mq; cq.N = qd; cq.K = D; cq.epi = EPI_HEADPOST;
+            cq.hp.B = Bq; cq.hp.S = S; cq.hp.nq = H; cq.hp.qw = ly.cqn; cq.hp.q = h->Qh; cq.hp.S_dst = S;
+            cq.hp.eps = eps;
+            RUN(hgemm(h, cq, s));
+            RUN(timed(h, 6, s, [&] {
+                return attention(h->Qh, h->Kc + l * cper, h->Vc + l * cper, h->AO, Bq, H, KV, S, Le, -1, scale, qd,
+                                 h->attn_ws, s);
+            }));
+            GemmArgs co{};
+            co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
+            co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
+            RUN(timed(h, 3, s, [&] { return hgemm(h, co, s, fuse_rowadd ? &pend : nullptr); }));
+        }
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533); the null rows' constant cross-O output
         // is added inside the norm pass (ACEHIP_FUSE_ROWADD=0: separate add_row_bcast, A/B)
-        RowAdd ra{};
+        RowAdd ra = pend;   // rows < ra.prows: the deferred cross-O (or O) epilogue, applied first
+        pend = RowAdd{};
         if (Mq < M) {
-            if (fuse_rowadd) ra = RowAdd{h->X, h->cnull + (size_t)l * D, Mq};
-            else RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
+            if (fuse_rowadd) {
+                ra.xw = h->X;
+                ra.v = h->cnull + (size_t)l * D;
+                ra.from = Mq;
+            } else {
+                RUN(add_row_bcast(h->X + (size_t)Mq * D, h->cnull + (size_t)l * D, M - Mq, D, s));
+            }
         }
         RUN(rmsnorm_mod(h->X, ly.n_mlp, md + 3 * D, md + 4 * D, mbs, S, h->XN, M, D, eps, s, ra));
         GemmArgs gu{};
@@ -798,10 +814,10 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
-        RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s); }));
+        RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr); }));
     }
     // norm_out AdaLN (base:1491-1497); proj_out runs after the body
-    RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s));
+    RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s, pend));
 #undef RUN
     return 0;
 }

@@ -1497,6 +1497,14 @@ static int splitk_fill() {
 }
 
 static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipStream_t s);
+// the split-K epilogue folded into its consumer (head_post for EPI_HEADPOST; the next
+// rmsnorm_mod for the residual epilogues, gemm(..., defer)): ACEHIP_SPLITK_FUSE=0 keeps
+// the separate splitk_epilogue_kernel launch (A/B); read per call
+static bool splitk_fuse_on() {
+    const char *e = getenv("ACEHIP_SPLITK_FUSE");
+    return !(e && e[0] == '0');
+}
+static bool splitk_hp_fused() { return splitk_fuse_on(); }
 
 // Skinny path (M ≤ 256, K % 128 == 0, N % 64 == 0): skinny_kernel<8, 4> over
 // ⌈M/128⌉ row chunks × N/64 slabs × `splits` K-ranges, splits chosen so the grid is
@@ -1541,7 +1549,7 @@ static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0) {
     return splitk_finish(a, a, splits, s);
 }
 
-static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
+static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s, RowAdd *defer = nullptr) {
     GemmArgs p = a;
     const int nk = a.K / BK;
     p.kper = (nk + splits - 1) / splits;
@@ -1550,12 +1558,33 @@ static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s) {
     if (splitk_stages(a.N) == 3) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     HIP_TRY(hipGetLastError());
+    if (defer) {
+        // the residual epilogue is left to the consumer norm (in place: C == res)
+        defer->xw = a.C;
+        defer->part = (const float *)a.ws;
+        defer->splits = splits;
+        defer->prows = a.M;
+        defer->plane = (int64_t)a.M * a.N;
+        defer->gate = a.epi == EPI_GATED_RES ? a.gate : nullptr;
+        defer->gate_bstride = a.gate_bstride;
+        defer->gate_rpb = a.epi == EPI_GATED_RES ? a.rows_per_batch : 1;
+        return 0;
+    }
     return splitk_finish(a, p, splits, s);
 }
 
 // sum the fp32 split partials in order + the GEMM's epilogue (head-post: staged bf16
 // projection + the standalone head_post kernel)
 static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipStream_t s) {
+    if (a.epi == EPI_HEADPOST && splitk_hp_fused()) {
+        // head_post reads the partials itself (one launch, no bf16 staging round trip)
+        HeadPostArgs h = a.hp;
+        h.part = (const float *)a.ws;
+        h.splits = splits;
+        h.plane = (int64_t)a.M * a.N;
+        h.ld_src = a.N;
+        return head_post(h, s);
+    }
     bf16_t *out = a.C;
     int64_t ldo = a.ldc;
     if (a.epi == EPI_HEADPOST) {   // bf16 projection staged after the partials
@@ -1687,7 +1716,8 @@ int gemm_small(const GemmArgs &a, int mode, hipStream_t s) {
     return gemm_splitk(a, splits, s);
 }
 
-int gemm(const GemmArgs &a, hipStream_t s) {
+int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
+    if (defer) defer->part = nullptr;
     if (a.M <= 0) return 0;
     // argument checks shared by every path (split-K included)
     if (a.N % 128 || a.K % BK || a.K <= 0)
@@ -1715,7 +1745,10 @@ int gemm(const GemmArgs &a, hipStream_t s) {
             int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4),
                                                 (splitk_fill() * cus + tiles - 1) / tiles);
             const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
-            if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s);
+            // a deferred epilogue needs the in-place residual form the consumer norm applies
+            const bool dfr = defer && splitk_fuse_on() && (a.epi == EPI_GATED_RES || a.epi == EPI_RES) &&
+                             a.res == a.C && a.ldr == a.ldc && a.ldc == a.N;
+            if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s, dfr ? defer : nullptr);
         }
     }
     if (a.epi == EPI_HEADPOST) {

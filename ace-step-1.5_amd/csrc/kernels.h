@@ -15,6 +15,9 @@ struct HeadPostArgs {
     bf16_t *q, *k, *v;                   // [B][nq|nk|nv][S_dst][128]
     int S_dst;
     float eps;
+    // split-K input (gemm's small-M path): the projection is Σ_s part[s·plane + row·ld_src + col]
+    // (fp32 partials summed in split order, then rounded to bf16) instead of src
+    const float *part = nullptr; int splits = 0; int64_t plane = 0;
 };
 enum GemmEpi {
     EPI_STORE = 0,       // C = bf16(acc + bias)
@@ -48,7 +51,11 @@ constexpr int EPI_PARTIAL = 5;
 constexpr int SK_MAX_BLOCKS = 256;
 constexpr size_t SK_PART_BYTES = (size_t)SK_MAX_BLOCKS << 18;   // 256 KiB per block
 constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace      // internal: store the fp32 accumulators of split blockIdx.y to ws
-int gemm(const GemmArgs &a, hipStream_t s);
+struct RowAdd;
+// defer != null: a residual-epilogue GEMM (EPI_GATED_RES / EPI_RES) that takes the small-M
+// split-K path leaves its fp32 partials in a.ws and describes its epilogue in *defer (the
+// consumer rmsnorm_mod applies it, one launch fewer); defer->part stays null otherwise
+int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer = nullptr);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
 int gemm_small(const GemmArgs &a, int mode, hipStream_t s);        // small-M A/B (needs ws)
 int gemm_sk_forced(const GemmArgs &a, hipStream_t s);              // stream-K 256² tile (needs sk_*)
@@ -90,6 +97,15 @@ struct RowAdd {
     bf16_t *xw = nullptr;
     const bf16_t *v = nullptr;
     int from = 0;
+    // deferred split-K residual epilogue (gemm(..., defer)): rows < prows first become
+    // x = bf16(x + bf16(bf16(acc)·gate[row / gate_rpb])) (gate != null) or bf16(x + bf16(acc)),
+    // acc = Σ_s part[s·plane + row·D + col] in split order — the splitk epilogue's arithmetic
+    const float *part = nullptr;
+    int splits = 0, prows = 0;
+    int64_t plane = 0;
+    const bf16_t *gate = nullptr;
+    int64_t gate_bstride = 0;
+    int gate_rpb = 1;
 };
 // rows_per_wave: kernel variant (tests / micro-bench: 1, 2, 4 rows per wave, −2 / −4 waves
 // per row); 0 = the default (1)

@@ -56,6 +56,42 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *x,   // 
 #pragma unroll
         for (int i = 0; i < NV; ++i) xr[r][i] = *(const vec_t *)(xp + (i * 64 + lane) * V);
     }
+    // rows < ra.prows first get the deferred split-K residual epilogue of the GEMM that
+    // produced them (gemm(..., defer)): x = bf16(x + bf16(bf16(Σ partials)·gate)) or
+    // bf16(x + bf16(Σ partials)), summed in split order as splitk_epilogue_kernel does
+    if (ra.part) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = row0 + r;
+            if (row >= M || row >= ra.prows) continue;   // wave-uniform
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int e = (i * 64 + lane) * V;
+                float xv[V], acc[V];
+                unpackv<V>(xr[r][i], xv);
+                const float *pp = ra.part + (int64_t)row * D + e;
+                if constexpr (V == 8) {
+                    sum_parts8(pp, ra.plane, ra.splits, acc);
+                } else {
+                    f32x4 t = *(const f32x4 *)pp;
+                    for (int sp = 1; sp < ra.splits; ++sp) t += *(const f32x4 *)(pp + sp * ra.plane);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[c] = t[c];
+                }
+                if (ra.gate) {
+                    float gg[V];
+                    unpackv<V>(*(const vec_t *)(ra.gate + (int64_t)(row / ra.gate_rpb) * ra.gate_bstride + e), gg);
+#pragma unroll
+                    for (int j = 0; j < V; ++j) xv[j] = xv[j] + rbf(rbf(acc[j]) * gg[j]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) xv[j] = xv[j] + rbf(acc[j]);
+                }
+                xr[r][i] = packv<V>(xv);
+                *(vec_t *)(ra.xw + (int64_t)row * D + e) = xr[r][i];
+            }
+        }
+    }
     // rows >= ra.from first get x = bf16(x + v), written back (the CFG null rows' constant
     // cross-attention output, add_row_bcast folded into this pass)
     if (ra.v) {
@@ -141,24 +177,60 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *x,   // 
 
 // WPR waves per row (D = 512·NV·WPR, 16-B accesses): more waves in flight
 // for the same bytes; the row's sum of squares is combined through LDS.
+// RowAdd (partials / row constant) as in rmsnorm_mod_kernel: the short-song path (few rows,
+// split-K partials to fold in) uses this kernel with WPR = 4 for more loads in flight per row
 template <int NV, int WPR>
-__global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *__restrict__ x,
+__global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *x,   // not restrict: RowAdd writes it
                                                             const bf16_t *__restrict__ w,
                                                             const bf16_t *__restrict__ shift,
                                                             const bf16_t *__restrict__ scale,
                                                             int64_t mod_bstride, int rows_per_batch,
                                                             bf16_t *__restrict__ out, int M, int D,
-                                                            float eps) {
+                                                            float eps, RowAdd ra) {
     constexpr int RPB = 4 / WPR;   // rows per 256-thread block
-    __shared__ float part[4];
+    __shared__ float run[4][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int rl = wave / WPR, wp = wave % WPR;
+    const bool live = blockIdx.x * RPB + rl < M;
     const int row = min(blockIdx.x * RPB + rl, M - 1);
     const int b = row / rows_per_batch;
     const bf16_t *xp = x + (int64_t)row * D;
     uint4 xr[NV], wr[NV], s1r[NV], s2r[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) xr[i] = *(const uint4 *)(xp + ((wp * NV + i) * 64 + lane) * 8);
+    if (ra.part && row < ra.prows) {               // wave-uniform
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int e = ((wp * NV + i) * 64 + lane) * 8;
+            float xv[8], acc[8];
+            unpack8(xr[i], xv);
+            sum_parts8(ra.part + (int64_t)row * D + e, ra.plane, ra.splits, acc);
+            if (ra.gate) {
+                float gg[8];
+                unpack8(*(const uint4 *)(ra.gate + (int64_t)(row / ra.gate_rpb) * ra.gate_bstride + e), gg);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = xv[j] + rbf(rbf(acc[j]) * gg[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = xv[j] + rbf(acc[j]);
+            }
+            xr[i] = pack8(xv);
+            if (live) *(uint4 *)(ra.xw + (int64_t)row * D + e) = xr[i];
+        }
+    }
+    if (ra.v && row >= ra.from) {                  // wave-uniform
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int e = ((wp * NV + i) * 64 + lane) * 8;
+            float xv[8], av[8];
+            unpack8(xr[i], xv);
+            unpack8(*(const uint4 *)(ra.v + e), av);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] += av[j];
+            xr[i] = pack8(xv);
+            if (live) *(uint4 *)(ra.xw + (int64_t)row * D + e) = xr[i];
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         const int e = ((wp * NV + i) * 64 + lane) * 8;
@@ -168,20 +240,28 @@ __global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *__rest
             s2r[i] = *(const uint4 *)(shift + (int64_t)b * mod_bstride + e);
         }
     }
+    // lane L's running sum of squares continues across the row's waves in element order
+    // (wave wp holds the lane's elements wp·NV·512 + …), then the same xor tree: exactly the
+    // fma sequence of the one-wave-per-row kernel, so both round identically
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        float f[8];
-        unpack8(xr[i], f);
+    for (int k = 0; k < WPR; ++k) {
+        if (wp == k) {                             // wave-uniform
+            ss = k == 0 ? 0.f : run[rl * WPR + k - 1][lane];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+            for (int i = 0; i < NV; ++i) {
+                float f[8];
+                unpack8(xr[i], f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+            }
+            run[rl * WPR + k][lane] = ss;
+        }
+        __syncthreads();
     }
-    ss = wave_sum(ss);
-    if (lane == 0) part[wave] = ss;
-    __syncthreads();
-    ss = 0.f;
+    ss = run[rl * WPR + WPR - 1][lane];
 #pragma unroll
-    for (int q = 0; q < WPR; ++q) ss += part[rl * WPR + q];   // fixed order: identical in every wave of the row
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
     if (blockIdx.x * RPB + rl >= M) return;
     const float rn = 1.0f / sqrtf(ss / (float)D + eps);
 #pragma unroll
@@ -212,16 +292,28 @@ __global__ __launch_bounds__(256) void head_post_kernel(HeadPostArgs a) {
     const int b = row / a.S, s = row % a.S;
     const int units = a.nq + a.nk + a.nv;
     const bf16_t *src = a.src + (int64_t)row * a.ld_src;
+    const float *psrc = a.part ? a.part + (int64_t)row * a.ld_src : nullptr;
     const int d = li * 8;
     float cs[8] = {}, sn[8] = {};
     if (a.cos) {
         unpack8(*(const uint4 *)(a.cos + (int64_t)s * 128 + d), cs);
         unpack8(*(const uint4 *)(a.sin + (int64_t)s * 128 + d), sn);
     }
-    for (int u0 = wave * 4; u0 < units; u0 += 16) {
+    for (int u0 = blockIdx.y * 16 + wave * 4; u0 < units; u0 += 16 * gridDim.y) {
         const int u = u0 + sub;
         float x[8] = {};
-        if (u < units) unpack8(*(const uint4 *)(src + u * 128 + d), x);
+        if (u < units) {
+            if (psrc) {
+                // split-K partials summed in split order, + 0 and bf16-rounded exactly as
+                // splitk_epilogue_kernel stages them (EPI_HEADPOST: no bias)
+                float acc[8];
+                sum_parts8(psrc + u * 128 + d, a.plane, a.splits, acc);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = rbf(acc[j] + 0.f);
+            } else {
+                unpack8(*(const uint4 *)(src + u * 128 + d), x);
+            }
+        }
         const bf16_t *nw;
         bf16_t *dst = head_dst(a, u, b, s, nw);
         float w[8] = {};
@@ -269,15 +361,18 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
                 hipStream_t s, RowAdd ra, int rows_per_wave) {
     if (M <= 0) return 0;
-    if (ra.v && (!ra.xw || ra.xw != x)) return fail(-1, "rmsnorm: row add must write back to x");
+    if ((ra.v || ra.part) && (!ra.xw || ra.xw != x)) return fail(-1, "rmsnorm: row add must write back to x");
+    if (ra.part && (ra.splits < 1 || ra.prows > M || ra.plane < (int64_t)ra.prows * D || ra.gate_rpb <= 0))
+        return fail(-1, "rmsnorm: deferred split-K epilogue arguments");
     if (D % 256 || D > 4096) return fail(-1, "rmsnorm: D must be a multiple of 256, <= 4096");
     if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
     const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
-    const int R = rows_per_wave ? rows_per_wave : 1;
-    if (R < 0 && !ra.v && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
+    // a deferred split-K epilogue (few rows, up to 16 partial slabs per row): 4 waves per row
+    const int R = rows_per_wave ? rows_per_wave : (ra.part && D % 2048 == 0 ? -4 : 1);
+    if (R < 0 && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
         const int WPR = -R, nv = D / (512 * WPR), grid = (M + 4 / WPR - 1) / (4 / WPR);
 #define SPLIT(NV_, W_) \
-    rmsnorm_split_kernel<NV_, W_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps)
+    rmsnorm_split_kernel<NV_, W_><<<grid, 256, 0, s>>>(x, w, shift, scale, mod_bstride, rpb, out, M, D, eps, ra)
         if (WPR == 2) {
             if (nv == 1) SPLIT(1, 2); else if (nv == 2) SPLIT(2, 2); else if (nv == 3) SPLIT(3, 2); else SPLIT(4, 2);
         } else {
@@ -298,7 +393,9 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
 
 int head_post(const HeadPostArgs &a, hipStream_t s) {
     if (a.B * a.S <= 0) return 0;
-    head_post_kernel<<<a.B * a.S, 256, 0, s>>>(a);
+    // reading split-K partials: one block per (row, 16 heads), more loads in flight per row
+    const int units = a.nq + a.nk + a.nv;
+    head_post_kernel<<<dim3(a.B * a.S, a.part ? (units + 15) / 16 : 1), 256, 0, s>>>(a);
     HIP_TRY(hipGetLastError());
     return 0;
 }

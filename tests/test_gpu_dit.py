@@ -755,3 +755,55 @@ def test_forward_step_matches_forward(gpu_device, graph):
     with pytest.raises(RuntimeError):
         rt.forward_step(xt, ctx, n)                  # outside the schedule
     rt.close()
+
+
+def _small_m_cfg():
+    # the real width (K = 2048 / 4096: ≥ 8 K-tiles, so the short-song GEMMs take the split-K
+    # path, and D = 2048 puts the deferred-epilogue norm on its 4-waves-per-row kernel)
+    return DiTConfig(hidden_size=2048, intermediate_size=4096, num_hidden_layers=3, num_attention_heads=16,
+                     num_key_value_heads=8, head_dim=128, sliding_window=16)
+
+
+@pytest.mark.parametrize("mode", ["turbo", "cfg", "null_only"])
+def test_splitk_epilogue_fused_into_consumers(gpu_device, monkeypatch, mode):
+    """Short songs (M = Bc·S ≤ 256): every projection runs on the split-K path; its epilogue is
+    folded into the consumer — head_post reads the QKV / cross-Q partials, and the residual
+    epilogues of O, cross-O and down are applied by the next RMSNorm pass (gemm(..., defer)).
+    Bit-identical to the separate splitk_epilogue_kernel launches (ACEHIP_SPLITK_FUSE=0), for
+    turbo (Bc = 1), the CFG pair with closed-form null rows + layer-0 dedup, and a condition
+    whose every row is the null row (no cross-attention at all); turbo also vs the oracle."""
+    from acehip.dit import DiTRuntime
+    cfg = _small_m_cfg()
+    W = synth_dit_weights(cfg, seed=17, mode="parity")
+    g = torch.Generator().manual_seed(5)
+    T, Lenc = 181, 37
+    xt = torch.randn(1, T, 64, generator=g).bfloat16()
+    ctx = torch.randn(1, T, 128, generator=g).bfloat16()
+    enc = torch.randn(1, Lenc, cfg.hidden_size, generator=g).bfloat16()
+    null = torch.randn(1, 1, cfg.hidden_size, generator=g).bfloat16().expand_as(enc)
+    rt = DiTRuntime(cfg, 0, max_S=128, max_Bc=2, max_Lenc=64)
+    rt.load({k: v.to(gpu_device, torch.bfloat16) for k, v in W.items()})
+    if mode == "turbo":
+        rt.set_condition(enc.to(gpu_device))
+    elif mode == "cfg":
+        rt.set_condition(torch.cat([enc, null]).to(gpu_device))
+        rt.set_uniform_rows(1)
+    else:
+        rt.set_condition(null.contiguous().to(gpu_device))
+        rt.set_uniform_rows(0)
+    t = torch.tensor([0.6], dtype=torch.float32, device=gpu_device)
+    x_d, c_d = xt.to(gpu_device), ctx.to(gpu_device)
+    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "0")
+    sep = rt.forward(x_d, c_d, t).clone()
+    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "1")
+    fused = rt.forward(x_d, c_d, t)
+    torch.cuda.synchronize()
+    assert torch.equal(sep, fused)
+    if mode == "turbo":
+        Wb = {k: v.bfloat16() for k, v in W.items()}
+        tb = torch.tensor([0.6], dtype=torch.bfloat16)
+        with torch.no_grad():
+            ref = dit_oracle.dit_forward(Wb, cfg, xt, tb, tb, enc, ctx).float()
+        out = fused.float().cpu()
+        assert rel_l2(out, ref) <= TOL_REL and cosine(out, ref) >= TOL_COS
+    rt.close()

@@ -111,9 +111,11 @@ def test_rmsnorm_variants_vs_oracle(gpu_device, D, mod):
             6 * D, rpb, ff.ptr(out), M, D, 1e-6, r, ff.stream_ptr()), "rmsnorm")
         outs.append(out)
     torch.cuda.synchronize()
-    for o in outs[1:3]:
-        assert torch.equal(o, outs[0])          # rows-per-wave changes scheduling, not arithmetic
-    for o in (outs[0], outs[3], outs[4]):       # waves-per-row also changes the fp32 sum order
-        got = o.cpu()
-        assert rel_l2(got.float(), ref.float()) < 2e-3
-        assert (got != ref).float().mean().item() < 1e-3
+    # rows-per-wave changes scheduling, not arithmetic; the waves-per-row kernel (the
+    # deferred split-K epilogue's norm) continues each lane's sum of squares across its waves
+    # in element order, so it rounds identically too
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    got = outs[0].cpu()
+    assert rel_l2(got.float(), ref.float()) < 2e-3
+    assert (got != ref).float().mean().item() < 1e-3

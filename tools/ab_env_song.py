@@ -2,7 +2,8 @@
 """DiT part of a 240 s song (27 CFG steps through AceStepDiTBackend.generate_audio) timed
 under several environment settings, interleaved in ONE process.
 
-usage: ab_env_song.py 'NAME=VAL[,NAME=VAL]' ['...' ...]   (first = baseline)"""
+usage: ab_env_song.py 'NAME=VAL[,NAME=VAL]' ['...' ...]   (first = baseline)
+SONG_SECONDS (default 240) and SONG_TURBO=1 (8 turbo steps, Bc = 1, no CFG) pick the song."""
 import os
 import statistics
 import sys
@@ -18,20 +19,24 @@ from acehip.weights import synth_dit_weights  # noqa: E402
 settings = [dict(kv.split("=") for kv in a.split(",") if kv) for a in sys.argv[1:]] or [{}]
 dev = torch.device("cuda:0")
 cfg = DiTConfig()
-T = 6000
-S = T // 2
+T = int(float(os.environ.get("SONG_SECONDS", "240")) * 25)
+S = (T + 1) // 2
+TURBO = os.environ.get("SONG_TURBO", "0") == "1"
 W = synth_dit_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch")
 rt = DiTRuntime(cfg, 0, max_S=S, max_Bc=2, max_Lenc=641)
 rt.load(W)
 del W
 g = torch.Generator(device=dev).manual_seed(0)
 null = torch.randn(1, 1, cfg.hidden_size, device=dev, generator=g).bfloat16()
-be = AceStepDiTBackend(rt, null, is_turbo=False)
+be = AceStepDiTBackend(rt, null, is_turbo=TURBO)
 enc = torch.randn(1, 641, cfg.hidden_size, device=dev, generator=g).bfloat16()
 ctx = torch.randn(1, T, 128, device=dev, generator=g).bfloat16()
 
 
 def song():
+    if TURBO:
+        return be.generate_audio(encoder_hidden_states=enc, context_latents=ctx, infer_steps=8, shift=3.0,
+                                 seed=1)["target_latents"]
     return be.generate_audio(encoder_hidden_states=enc, context_latents=ctx, infer_steps=27,
                              diffusion_guidance_sale=7.0, shift=3.0, seed=1)["target_latents"]
 
@@ -42,7 +47,7 @@ for st in settings:
     outs.append(song().float().clone())
     for k in st:
         os.environ.pop(k)
-for _ in range(3):
+for _ in range(int(os.environ.get("ROUNDS", "3"))):
     for i, st in enumerate(settings):
         os.environ.update(st)
         torch.cuda.synchronize()
