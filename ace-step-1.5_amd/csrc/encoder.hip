@@ -58,12 +58,12 @@ struct acehip_enc {
 };
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
-static inline int hgemm(acehip_enc *h, GemmArgs g, hipStream_t s) {
+static inline int hgemm(acehip_enc *h, GemmArgs g, hipStream_t s, RowAdd *defer = nullptr) {
     g.ws = h->gemm_ws;
     g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
     g.sk_part = h->sk_part;
     g.sk_flag = h->sk_flag;
-    return gemm(g, s);
+    return gemm(g, s, defer);
 }
 
 namespace {
@@ -276,9 +276,13 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
     int rc;
 #define RUN(e) do { if ((rc = (e))) return rc; } while (0)
     HIP_TRY(hipMemcpyAsync(h->X, x, (size_t)M * D * 2, hipMemcpyDeviceToDevice, s));
+    // few tokens (text / lyric encoders): the O and down GEMMs take gemm's split-K path and
+    // leave their residual epilogue to the next norm (`pend`, as in the DiT forward)
+    RowAdd pend{};
     for (int l = 0; l < h->L; ++l) {
         const auto &ly = h->layers[l];
-        RUN(rmsnorm_mod(h->X, ly.ln1, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
+        RUN(rmsnorm_mod(h->X, ly.ln1, nullptr, nullptr, 0, S, h->XN, M, D, eps, s, pend));
+        pend = RowAdd{};
         GemmArgs q{};
         q.A = h->XN; q.lda = D; q.W = ly.wqkv; q.ldw = D;
         q.M = M; q.N = qd + 2 * kvd; q.K = D; q.epi = EPI_HEADPOST;
@@ -292,8 +296,9 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
         GemmArgs o{};
         o.A = h->AO; o.lda = qd; o.W = ly.wo; o.ldw = qd; o.C = h->X; o.ldc = D;
         o.M = M; o.N = D; o.K = qd; o.epi = EPI_RES; o.res = h->X; o.ldr = D;
-        RUN(hgemm(h, o, s));
-        RUN(rmsnorm_mod(h->X, ly.ln2, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
+        RUN(hgemm(h, o, s, &pend));
+        RUN(rmsnorm_mod(h->X, ly.ln2, nullptr, nullptr, 0, S, h->XN, M, D, eps, s, pend));
+        pend = RowAdd{};
         GemmArgs gu{};
         gu.A = h->XN; gu.lda = D; gu.W = ly.wgu; gu.ldw = D; gu.C = h->Hb; gu.ldc = F;
         gu.M = M; gu.N = 2 * F; gu.K = D; gu.epi = EPI_SWIGLU;
@@ -301,14 +306,14 @@ int acehip_enc_forward(acehip_enc *h, const void *x, const uint8_t *kmask, int B
         GemmArgs dn{};
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_RES; dn.res = h->X; dn.ldr = D;
-        RUN(hgemm(h, dn, s));
+        RUN(hgemm(h, dn, s, &pend));
     }
     if (!h->cfg.out_dim) {
-        RUN(rmsnorm_mod(h->X, h->norm, nullptr, nullptr, 0, S, (bf16_t *)out, M, D, eps, s));
+        RUN(rmsnorm_mod(h->X, h->norm, nullptr, nullptr, 0, S, (bf16_t *)out, M, D, eps, s, pend));
         return 0;
     }
     // detokenizer proj_out (base:991): rows padded to 128 with zeros, then the used columns
-    RUN(rmsnorm_mod(h->X, h->norm, nullptr, nullptr, 0, S, h->XN, M, D, eps, s));
+    RUN(rmsnorm_mod(h->X, h->norm, nullptr, nullptr, 0, S, h->XN, M, D, eps, s, pend));
     GemmArgs po{};
     po.A = h->XN; po.lda = D; po.W = h->wout; po.ldw = D; po.C = h->O128; po.ldc = 128;
     po.M = M; po.N = 128; po.K = D; po.epi = EPI_STORE; po.bias = h->bout;

@@ -368,7 +368,7 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
     if ((shift == nullptr) != (scale == nullptr)) return fail(-1, "rmsnorm: shift/scale");
     const int rpb = rows_per_batch > 0 ? rows_per_batch : M;
     // a deferred split-K epilogue (few rows, up to 16 partial slabs per row): 4 waves per row
-    const int R = rows_per_wave ? rows_per_wave : (ra.part && D % 2048 == 0 ? -4 : 1);
+    const int R = rows_per_wave ? rows_per_wave : !ra.part ? 1 : D % 2048 == 0 ? -4 : D % 1024 == 0 ? -2 : 1;
     if (R < 0 && D % (512 * -R) == 0 && D / (512 * -R) <= 4) {   // -WPR: WPR waves per row
         const int WPR = -R, nv = D / (512 * WPR), grid = (M + 4 / WPR - 1) / (4 / WPR);
 #define SPLIT(NV_, W_) \

@@ -56,3 +56,32 @@ def test_text_encoder_hip_vs_transformers(gpu_device, tag):
     assert cosine(out.float().cpu(), ref) >= TOL_COS
     assert torch.equal(emb.cpu(), torch.nn.functional.embedding(ids.cpu(), W["embed_tokens.weight"].bfloat16()))
     te.close()
+
+
+@pytest.mark.gpu
+def test_text_encoder_real_width_splitk_fusion(gpu_device, monkeypatch):
+    """The real Qwen3-0.6B width (D = 1024, F = 3072; 3 of its 28 layers) at 128 tokens: the
+    O / down GEMMs take the split-K path and their residual epilogue is applied by the next
+    RMSNorm (2 waves per row).  Bit-identical to the separate split-K epilogue launches
+    (ACEHIP_SPLITK_FUSE=0), and within the bf16 tolerance of the oracle."""
+    from acehip.condition import TextEncoder
+    from acehip.config import DiTConfig
+    from acehip.weights import synth_text_encoder_weights
+    from oracle import condenc_oracle
+    cfg = DiTConfig(**dict(TextEncoder.QWEN3_06B, num_hidden_layers=3))
+    W = synth_text_encoder_weights(cfg, 300, seed=4, mode="parity")
+    te = TextEncoder(cfg, device=gpu_device.index or 0, max_batch=1, max_tokens=256)
+    te.load({k: v.to(gpu_device) for k, v in W.items()})
+    ids = torch.randint(0, 300, (1, 128), generator=torch.Generator().manual_seed(9)).to(gpu_device)
+    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "0")
+    sep = te(input_ids=ids).last_hidden_state.clone()
+    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "1")
+    fused = te(input_ids=ids).last_hidden_state
+    torch.cuda.synchronize()
+    assert torch.equal(sep, fused)
+    Wb = {k: v.bfloat16() for k, v in W.items()}
+    with torch.no_grad():
+        ref = condenc_oracle.text_encoder(Wb, cfg, ids.cpu()).float()
+    out = fused.float().cpu()
+    assert rel_l2(out, ref) <= TOL_REL and cosine(out, ref) >= TOL_COS
+    te.close()
