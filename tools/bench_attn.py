@@ -19,7 +19,8 @@ from acehip import _ffi as ff  # noqa: E402
 
 dev = torch.device("cuda:0")
 S = int(os.environ.get("ATTN_S", "3000"))
-SHAPES = {"full": (2, 16, 8, S, S, -1), "band": (2, 16, 8, S, S, 128), "cross": (2, 16, 8, S, 641, -1),
+B0 = int(os.environ.get("ATTN_B", "2"))
+SHAPES = {"full": (B0, 16, 8, S, S, -1), "band": (B0, 16, 8, S, S, 128), "cross": (B0, 16, 8, S, 641, -1),
           "cross1": (1, 16, 8, S, 641, -1)}
 if os.environ.get("SHAPES"):
     SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
