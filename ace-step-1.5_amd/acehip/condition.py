@@ -193,17 +193,24 @@ def _rope_theta(c) -> float:
     return float(rp.get("rope_theta", getattr(c, "rope_theta", 1_000_000.0)))
 
 
-def unpack_timbre(emb: torch.Tensor, order: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def timbre_layout(order: torch.Tensor) -> Tuple[int, int]:
+    """(batch size, max references per song) of a packed-timbre order vector (host values)."""
+    o = order.long().flatten().tolist()
+    B = max(o) + 1
+    return B, max(o.count(b) for b in range(B))
+
+
+def unpack_timbre(emb: torch.Tensor, order: torch.Tensor,
+                  layout: Optional[Tuple[int, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """AceStepTimbreEncoder.unpack_timbre_embeddings (base:1023-1073): packed rows
     [N, d] → [B, max_count, d] by batch id in packed order, mask [B, max_count] long.
     (The reference's one-hot matmul places each row exactly; an index scatter
-    is the same result.)"""
+    is the same result.)  `layout` = timbre_layout(order) when already known (no host sync)."""
     N, d = emb.shape
     dev = emb.device
     order = order.to(dev).long()
-    B = int(order.max().item()) + 1
+    B, max_count = layout if layout is not None else timbre_layout(order)
     counts = torch.bincount(order, minlength=B)
-    max_count = int(counts.max().item())
     sorted_idx = torch.argsort(order * N + torch.arange(N, device=dev), stable=True)
     starts = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(counts, 0)[:-1]])
     pos_sorted = torch.arange(N, device=dev) - starts[order[sorted_idx]]
@@ -279,10 +286,10 @@ class ConditionEncoder:
         """AceStepLyricEncoder.forward (base:603-731) → last_hidden_state."""
         return self.lyric.forward(self.lyric.embed(lyric_hidden_states), lyric_attention_mask)
 
-    def timbre_encoder(self, packed, order):
+    def timbre_encoder(self, packed, order, layout=None):
         """AceStepTimbreEncoder.forward (base:1076-1178): no padding mask, row 0."""
         h = self.timbre.forward(self.timbre.embed(packed), None)
-        return unpack_timbre(h[:, 0, :], order)
+        return unpack_timbre(h[:, 0, :], order, layout)
 
     def __call__(self, text_hidden_states, text_attention_mask, lyric_hidden_states, lyric_attention_mask,
                  refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask):

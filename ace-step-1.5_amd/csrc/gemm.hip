@@ -1491,6 +1491,10 @@ static int splitk_stages(int N) {
     const char *e = getenv("ACEHIP_SPLITK_STAGES");
     return e ? atoi(e) : (N <= 4096 ? 3 : 2);
 }
+static int splitk_min_ktiles() {   // fewest K-tiles per split (ACEHIP_SPLITK_MINK, A/B; read per call)
+    const char *e = getenv("ACEHIP_SPLITK_MINK");
+    return e ? std::max(1, atoi(e)) : 4;
+}
 static int splitk_fill() {
     const char *e = getenv("ACEHIP_SPLITK_FILL");
     return e ? std::max(1, atoi(e)) : 1;
@@ -1514,23 +1518,16 @@ static bool splitk_hp_fused() { return splitk_fuse_on(); }
 // QKV 17 vs 18, O 16 vs 16; even W-only streaming (M = 16) reaches 2.4 TB/s against
 // split-K's 2.9, and every shape carries a ~10 µs floor (two launches, the cold-weight
 // first touch) — so it is off by default; ACEHIP_SKINNY=1 selects it (A/B).
-static bool use_skinny() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("ACEHIP_SKINNY");
-        v = (e && e[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
+static bool use_skinny() {   // read per call (in-process A/B)
+    const char *e = getenv("ACEHIP_SKINNY");
+    return e && e[0] == '1';
 }
-static int skinny_depth() {   // register-ring depth (A/B knob ACEHIP_SKINNY_D = 2 | 3 | 4)
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("ACEHIP_SKINNY_D");
-        v = e ? atoi(e) : 3;
-    }
-    return v;
+static int skinny_depth() {   // register-ring depth (A/B knob ACEHIP_SKINNY_D = 2 | 3 | 4; read per call)
+    const char *e = getenv("ACEHIP_SKINNY_D");
+    return e ? atoi(e) : 3;
 }
-static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0) {
+static void fill_defer(const GemmArgs &a, int splits, RowAdd *defer);
+static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0, RowAdd *defer = nullptr) {
     constexpr int MT = 8, NT = 4, BN = 16 * NT;
     if (!depth) depth = skinny_depth();
     const int cus = num_cus();
@@ -1546,6 +1543,10 @@ static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0) {
     else if (depth == 2) skinny_kernel<MT, NT, 2><<<slabs * splits * nchunk, 256, 0, s>>>(a, kper, splits, nchunk);
     else skinny_kernel<MT, NT, 3><<<slabs * splits * nchunk, 256, 0, s>>>(a, kper, splits, nchunk);
     HIP_TRY(hipGetLastError());
+    if (defer) {
+        fill_defer(a, splits, defer);
+        return 0;
+    }
     return splitk_finish(a, a, splits, s);
 }
 
@@ -1559,18 +1560,22 @@ static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s, RowAdd *def
     else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     HIP_TRY(hipGetLastError());
     if (defer) {
-        // the residual epilogue is left to the consumer norm (in place: C == res)
-        defer->xw = a.C;
-        defer->part = (const float *)a.ws;
-        defer->splits = splits;
-        defer->prows = a.M;
-        defer->plane = (int64_t)a.M * a.N;
-        defer->gate = a.epi == EPI_GATED_RES ? a.gate : nullptr;
-        defer->gate_bstride = a.gate_bstride;
-        defer->gate_rpb = a.epi == EPI_GATED_RES ? a.rows_per_batch : 1;
+        fill_defer(a, splits, defer);
         return 0;
     }
     return splitk_finish(a, p, splits, s);
+}
+
+// the residual epilogue is left to the consumer norm (in place: C == res)
+static void fill_defer(const GemmArgs &a, int splits, RowAdd *defer) {
+    defer->xw = a.C;
+    defer->part = (const float *)a.ws;
+    defer->splits = splits;
+    defer->prows = a.M;
+    defer->plane = (int64_t)a.M * a.N;
+    defer->gate = a.epi == EPI_GATED_RES ? a.gate : nullptr;
+    defer->gate_bstride = a.gate_bstride;
+    defer->gate_rpb = a.epi == EPI_GATED_RES ? a.rows_per_batch : 1;
 }
 
 // sum the fp32 split partials in order + the GEMM's epilogue (head-post: staged bf16
@@ -1732,9 +1737,12 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
             h.S_dst < h.S || (h.nq && !h.qw) || (h.nk && !h.kw) || (h.cos == nullptr) != (h.sin == nullptr))
             return fail(-1, "gemm: head-post arguments inconsistent with the GEMM shape");
     }
+    // a deferred epilogue needs the in-place residual form the consumer norm applies
+    const bool dfr = defer && splitk_fuse_on() && (a.epi == EPI_GATED_RES || a.epi == EPI_RES) && a.res == a.C &&
+                     a.ldr == a.ldc && a.ldc == a.N;
     if (a.ws && a.M <= 256 && a.N % 64 == 0 && a.K % 128 == 0 && a.K >= 512 && use_skinny() &&
         (a.epi != EPI_SWIGLU || a.N % 64 == 0)) {
-        const int rc = gemm_skinny(a, s);
+        const int rc = gemm_skinny(a, s, 0, dfr ? defer : nullptr);
         if (rc <= 0) return rc;   // done (0) or failed (< 0); 1 = workspace too small
     }
     if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
@@ -1742,12 +1750,9 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
         const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
         const int nk = a.K / BK;
         if (tiles * 2 <= cus && nk >= 8) {
-            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / 4),
+            int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / splitk_min_ktiles()),
                                                 (splitk_fill() * cus + tiles - 1) / tiles);
             const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
-            // a deferred epilogue needs the in-place residual form the consumer norm applies
-            const bool dfr = defer && splitk_fuse_on() && (a.epi == EPI_GATED_RES || a.epi == EPI_RES) &&
-                             a.res == a.C && a.ldr == a.ldc && a.ldc == a.N;
             if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s, dfr ? defer : nullptr);
         }
     }
