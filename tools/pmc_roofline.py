@@ -34,9 +34,19 @@ def _short(name):
     return re.sub(r"\(.*\)$", "", name)
 
 
+# position of the EPI template argument per GEMM kernel (gemm.hip): gemm_pp_kernel<BM, EPI, DBG,
+# SPL, SCH>, gemm_w4_kernel<BM, BN, EPI, ...>, gemm_kernel<BM, BN, WM, WN, STAGES, EPI>,
+# gemm_sk_kernel<EPI>
+EPI_POS = {"gemm_pp_kernel": 1, "gemm_w4_kernel": 2, "gemm_kernel": 5, "gemm_sk_kernel": 0}
+
+
 def _is_swiglu(short):
     m = re.match(r"(gemm_\w*kernel)<(.*)>$", short)
-    return bool(m) and m.group(2).split(",")[-1].strip() == "3"
+    if not m or m.group(1) not in EPI_POS:
+        return False
+    args = [x.strip() for x in m.group(2).split(",")]
+    i = EPI_POS[m.group(1)]
+    return i < len(args) and args[i] == "3"
 
 
 def dispatches(db, counters):
