@@ -77,6 +77,7 @@ struct SplitArgs {
     int nq, full, nsplit;
     float *ws;     // ≥ (units − full)·nsplit·8·66·64 floats
     int *cnt;      // ≥ units − full ints, zero between launches
+    int units = 0; // attn_pw_kernel: > 0 = persistent over units [0, units) (no splits)
 };
 
 // ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
@@ -723,49 +724,84 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
     // one exec-masked sequence with both register sets live)
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
+    // persistent mode (sp.units > 0, band layers with more units than CUs): this workgroup runs
+    // units blockIdx.x, blockIdx.x + gridDim.x, ... as ONE stream of KV tiles — the next unit's
+    // first two tiles are staged during the current unit's last two, its Q is loaded behind the
+    // last tile's barrier and its first K reads ride in the last P·V phase, so a unit boundary
+    // costs the O write-out instead of a launch round's prologue (cost model, tools/attn_cost.py:
+    // ≈ 9 µs per round of units + ≈ 2 µs per tile)
+    const bool persist = sp.units > 0;
     int u = blockIdx.x, part = 0, nsplit = 1;
-    if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
-    if (u >= sp.full) {
-        const int j = u - sp.full;
-        u = sp.full + j / sp.nsplit;
-        part = j % sp.nsplit;
-        nsplit = sp.nsplit;
+    if (!persist) {
+        if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
+        if (u >= sp.full) {
+            const int j = u - sp.full;
+            u = sp.full + j / sp.nsplit;
+            part = j % sp.nsplit;
+            nsplit = sp.nsplit;
+        }
     }
-    const int qb = u % sp.nq, kvh = (u / sp.nq) % KV, b = u / (sp.nq * KV);
-    const int hq = 2 * kvh + (wave >> 1);
-    const int qblk = qb * QB;
-    const int q0 = qblk + (wave & 1) * 64;     // this wave's 64 rows: sub-block sb = rows q0 + 32·sb + r
-    const int qi[2] = {q0 + r, q0 + 32 + r};
+    // geometry of unit uu (wave-uniform)
+    struct UnitG {
+        int b, kvh, hq, q0, t_first, ntiles;
+    };
+    auto geom = [&](int uu, int pt, int ns) __attribute__((always_inline)) {
+        UnitG g;
+        const int qb = uu % sp.nq;
+        g.kvh = (uu / sp.nq) % KV;
+        g.b = uu / (sp.nq * KV);
+        g.hq = 2 * g.kvh + (wave >> 1);
+        const int qblk = qb * QB;
+        g.q0 = qblk + (wave & 1) * 64;     // this wave's 64 rows: sub-block sb = rows q0 + 32·sb + r
+        int kv_lo = 0, kv_hi = Sk;
+        if (window >= 0) {
+            kv_lo = max(0, qblk - window);
+            kv_hi = min(Sk, qblk + QB + window);
+        }
+        g.t_first = kv_lo / KT;
+        g.ntiles = (kv_hi + KT - 1) / KT - g.t_first;
+        if (ns > 1) {
+            const int per = (g.ntiles + ns - 1) / ns;
+            const int t0 = min(g.ntiles, pt * per), t1 = min(g.ntiles, t0 + per);
+            g.t_first += t0;
+            g.ntiles = t1 - t0;
+        }
+        return g;
+    };
+    // this wave's LDS-DMA source (waves 0-1 stage K, 2-3 V) of unit g's KV head, as SGPRs
+    auto kv_base = [&](const UnitG &g) __attribute__((always_inline)) {
+        const bf16_t *base = (wave < 2 ? k : v) + ((int64_t)g.b * KV + g.kvh) * (int64_t)Sk * 128;
+        return (const char *)pw_uniform(base);
+    };
+    // Q of unit g → AGPRs a[128:191]
+    auto load_q = [&](const UnitG &g) __attribute__((always_inline)) {
+        sfor<0, 2>([&](auto SB) __attribute__((always_inline)) {
+            constexpr int sb = decltype(SB)::value;
+            const bf16_t *qp = q + (((int64_t)g.b * H + g.hq) * Sq + min(g.q0 + 32 * sb + r, Sq - 1)) * 128 + 8 * hh;
+            sfor<0, 8>([&](auto S) __attribute__((always_inline)) {
+                pw_qload<PW_Q + 32 * sb + 4 * decltype(S)::value>(qp + 16 * decltype(S)::value);
+            });
+        });
+    };
+    // the loop carries only what the tile loop reads (t_first, ntiles, q0 of this unit; t_first,
+    // ntiles of the next): the rest is recomputed from the unit index where it is used — the
+    // whole-struct copy cost SGPR spills
+    int c_tf, c_nt, c_q0;
+    {
+        const UnitG g = geom(u, part, nsplit);
+        c_tf = g.t_first;
+        c_nt = g.ntiles;
+        c_q0 = g.q0;
+    }
+    int qi[2] = {c_q0 + r, c_q0 + 32 + r};
 
     // O = 0 and Q → AGPRs (the clobber of a0 / a255 makes the kernel descriptor allocate all 256)
     sfor<0, 128>([&](auto I) __attribute__((always_inline)) {
         asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "n"(PW_O + decltype(I)::value));
     });
     asm volatile("s_nop 0" ::: "a0", "a255");
-    sfor<0, 2>([&](auto SB) __attribute__((always_inline)) {
-        constexpr int sb = decltype(SB)::value;
-        const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi[sb], Sq - 1)) * 128 + 8 * hh;
-        sfor<0, 8>([&](auto S) __attribute__((always_inline)) {
-            pw_qload<PW_Q + 32 * sb + 4 * decltype(S)::value>(qp + 16 * decltype(S)::value);
-        });
-    });
+    load_q(geom(u, 0, 1));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
-    const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
-    int kv_lo = 0, kv_hi = Sk;
-    if (window >= 0) {
-        kv_lo = max(0, qblk - window);
-        kv_hi = min(Sk, qblk + QB + window);
-    }
-    int t_first = kv_lo / KT;
-    int ntiles = (kv_hi + KT - 1) / KT - t_first;
-    if (nsplit > 1) {
-        const int per = (ntiles + nsplit - 1) / nsplit;
-        const int t0 = min(ntiles, part * per), t1 = min(ntiles, t0 + per);
-        t_first += t0;
-        ntiles = t1 - t0;
-    }
     // 32 KiB tile = 32 LDS-DMA wave-instructions, 8 per wave
     // Whole tiles (kv0 + 64 ≤ Sk) go by the saddr form: SGPR base = K or V + the piece's first
     // key row (uniform: waves 0-1 stage K, 2-3 V), VGPR = the lane's swizzled 16-B slot, one of
@@ -777,14 +813,15 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         const int row = 4 * j + (lane >> 4);
         dma_off[j] = (uint32_t)((lane >> 4) * 256 + (((lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4));
     }
-    const char *kv_src = (const char *)pw_uniform(wave < 2 ? kp : vp);
+    const char *kv_src = kv_base(geom(u, 0, 1));
     const uint32_t lds_u = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
-    auto stage_tile = [&](int kv0, int buf) __attribute__((always_inline)) {
+    // tile at key kv0 of the KV head whose K (waves 0-1) or V (waves 2-3) base is src → ring slot buf
+    auto stage_tile = [&](const char *src, int kv0, int buf) __attribute__((always_inline)) {
         if (kv0 + KT <= Sk) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int c = wave * 8 + i;
-                pw_dma(kv_src + (int64_t)(kv0 + (c & 15) * 4) * 256, dma_off[i & 3],
+                pw_dma(src + (int64_t)(kv0 + (c & 15) * 4) * 256, dma_off[i & 3],
                        lds_u + ((c >> 4) * NBUF + buf) * TILE + (c & 15) * 1024);
             }
             return;
@@ -795,9 +832,13 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
             const int isv = c >> 4, row = (c & 15) * 4 + (lane >> 4), pc = lane & 15;
             const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
             const int key = min(kv0 + row, Sk - 1);
-            glds16((isv ? vp : kp) + (int64_t)key * 128 + ch * 8, lds + (isv * NBUF + buf) * TILE + (c & 15) * 1024);
+            glds16((const bf16_t *)src + (int64_t)key * 128 + ch * 8, lds + (isv * NBUF + buf) * TILE + (c & 15) * 1024);
         }
     };
+    // the unit after this one (persistent mode)
+    bool has_next = false;
+    int un = 0, n_tf = 0, n_nt = 0;
+    const char *nx_src = kv_src;
 
     const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
@@ -836,7 +877,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
     auto tile = [&](int it, auto SLOTC, auto MASKC, bool outside) __attribute__((always_inline)) {
         constexpr int SLOT = decltype(SLOTC)::value;
         constexpr int NSLOT = (SLOT + 1) % NBUF;
-        const int kv0 = (t_first + it) * KT;
+        const int kv0 = (c_tf + it) * KT;
         s16x4 rv[4][2][2][2];         // Vᵀ fragments of the current tile, per d-block
         f32x16 st[2][2];              // scores per sub-block and key half
         bf16x8 pf[2][2][2];           // P (bf16) per sub-block, B operand of P·V
@@ -973,10 +1014,18 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
 #if !PW_X_NOBAR
         tile_barrier();
 #endif
+        if (has_next && it == c_nt - 1) {
+            // the next unit's Q, behind the barrier that follows this unit's last QKᵀ MFMAs
+            // (s_nop: their AGPR reads before the loads' writes); it lands during this tile's
+            // P·V and the O write-out, waited for before the first QKᵀ of that unit
+            asm volatile("s_nop 7" ::: "memory");
+            load_q(geom(un, 0, 1));
+        }
 #if !PW_X_NODMA
-        if (it + 2 < ntiles) stage_tile(kv0 + 2 * KT, SLOT);
+        if (it + 2 < c_nt) stage_tile(kv_src, kv0 + 2 * KT, SLOT);
+        else if (has_next && it + 2 - c_nt < n_nt) stage_tile(nx_src, (n_tf + it + 2 - c_nt) * KT, SLOT);
 #endif
-        const bool more = it + 1 < ntiles;
+        const bool more = it + 1 < c_nt || has_next;
         if (!outside) {
             pf_fence(pf[0]);
             sfor<0, 16>([&](auto G) __attribute__((always_inline)) {     // phase 4
@@ -1000,23 +1049,31 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
     };
     // band: tiles outside the band of all 64 rows skipped; tiles inside it for all 64 mask-free
     auto run_tile = [&](int it, auto SLOTC) __attribute__((always_inline)) {
-        const int kv0 = (t_first + it) * KT;
+        const int kv0 = (c_tf + it) * KT, q0 = c_q0;
         const bool outside = window >= 0 && (kv0 > q0 + 63 + window || kv0 + KT - 1 < q0 - window);
         const bool interior = kv0 + KT <= Sk && (window < 0 || (kv0 >= q0 + 63 - window && kv0 + KT - 1 <= q0 + window));
         if (interior) tile(it, SLOTC, IC<0>{}, outside);
         else tile(it, SLOTC, IC<1>{}, outside);
     };
     // prologue: tile 0 staged and visible, tile 1 in flight, K(0) read
-    if (ntiles > 0) stage_tile(t_first * KT, 0);
+    if (c_nt > 0) stage_tile(kv_src, c_tf * KT, 0);
     tile_barrier();
-    if (ntiles > 1) stage_tile((t_first + 1) * KT, 1);
-    if (ntiles > 0) sfor<0, 16>([&](auto G) __attribute__((always_inline)) { k_read(IC<0>{}, G); });
-    int it = 0;
-    for (; it + 1 < ntiles; it += 2) {
-        run_tile(it, IC<0>{});
-        run_tile(it + 1, IC<1>{});
+    if (c_nt > 1) stage_tile(kv_src, (c_tf + 1) * KT, 1);
+    if (c_nt > 0) sfor<0, 16>([&](auto G) __attribute__((always_inline)) { k_read(IC<0>{}, G); });
+    int gpos = 0;   // position of the current tile in the workgroup's tile stream: ring slot gpos & 1
+    for (;;) {
+    un = u + (int)gridDim.x;
+    has_next = persist && un < sp.units;
+    if (has_next) {
+        const UnitG g = geom(un, 0, 1);
+        n_tf = g.t_first;
+        n_nt = g.ntiles;
+        nx_src = kv_base(g);
     }
-    if (it < ntiles) run_tile(it, IC<0>{});
+    for (int it = 0; it < c_nt; ++it, ++gpos) {
+        if (gpos & 1) run_tile(it, IC<1>{});
+        else run_tile(it, IC<0>{});
+    }
 
     // O out of the AGPRs (the last MFMAs wrote them just before: XDL → read pad)
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
@@ -1075,11 +1132,18 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         if (tid == 0) sp.cnt[u - sp.full] = 0;
     }
 
+    if (has_next) {
+        // the next unit's Q (16 loads) landed; only its tile-1 LDS-DMA (8 pieces, issued after
+        // the Q loads) may still be in flight — before any store joins the vmcnt queue
+        if (n_nt >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
         if (qi[sb] >= Sq) continue;            // both lanes of a row pair leave together
         const float inv = 1.0f / l[sb];
-        bf16_t *op = o + ((int64_t)b * Sq + qi[sb]) * o_ld + hq * 128;
+        const int ub = u / (sp.nq * KV), uhq = 2 * ((u / sp.nq) % KV) + (wave >> 1);
+        bf16_t *op = o + ((int64_t)ub * Sq + qi[sb]) * o_ld + uhq * 128;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -1095,6 +1159,21 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
                 *(uint4 *)(op + 32 * dt + 16 * gp + 8 * hh) = pack8(vv);
             }
     }
+    if (!has_next) break;
+    // next unit: O = 0 (its first P·V is a whole tile away), fresh softmax state
+    sfor<0, 128>([&](auto I) __attribute__((always_inline)) {
+        asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "n"(PW_O + decltype(I)::value));
+    });
+    m[0] = m[1] = NEG;
+    l[0] = l[1] = 0.f;
+    u = un;
+    c_tf = n_tf;
+    c_nt = n_nt;
+    c_q0 = (u % sp.nq) * QB + (wave & 1) * 64;
+    kv_src = nx_src;
+    qi[0] = c_q0 + r;
+    qi[1] = c_q0 + 32 + r;
+    }   // unit loop
 }
 
 }  // namespace
@@ -1161,7 +1240,15 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
             sp.cnt = (int *)ws;
             sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
         }
-        const int grid = sp.full + (units - sp.full) * sp.nsplit;
+        int grid = sp.full + (units - sp.full) * sp.nsplit;
+        // band layers with more units than CUs: one persistent workgroup per CU walking units
+        // blockIdx.x + k·grid as one KV-tile stream (every unit then has ≥ 2 tiles: window ≥ KT,
+        // Sq = Sk > 2·KT).  ACEHIP_ATTN_PERSIST=0 restores one workgroup per unit (A/B; per call)
+        const char *pe = getenv("ACEHIP_ATTN_PERSIST");
+        if (!(pe && pe[0] == '0') && sp.nsplit == 1 && window >= KT && Sq == Sk && Sq > 2 * KT && units > cus) {
+            sp.units = units;
+            grid = cus;
+        }
         attn_pw_kernel<<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
         HIP_TRY(hipGetLastError());
         return 0;

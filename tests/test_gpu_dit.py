@@ -101,6 +101,37 @@ def test_attention_tail_split(gpu_device, monkeypatch, cus, window, pw):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
+@pytest.mark.parametrize("cus,B,H,KV,S,window", [(16, 2, 4, 2, 1000, 128), (37, 2, 4, 2, 1000, 128),
+                                                  (100, 1, 16, 8, 777, 64), (7, 1, 2, 1, 450, 200),
+                                                  (0, 2, 16, 8, 3000, 128), (0, 4, 16, 8, 3000, 128)])
+def test_attention_band_persistent(gpu_device, monkeypatch, cus, B, H, KV, S, window):
+    """Band layers with more units than CUs run attn_pw_kernel persistently (one workgroup per
+    CU walking units blockIdx + k·grid as one KV-tile stream: the next unit's tiles staged during
+    the current unit's last two, its Q loaded behind the last tile's barrier).  ACEHIP_ATTN_CUS
+    shrinks the grid so small shapes walk 2..10 units per workgroup (odd tile counts flip the
+    ring parity between units; ragged S leaves a partial last tile); cus = 0 keeps the real
+    CU count (the 240 s / 2- and 3-round shapes).  Bit-identical to one workgroup per unit."""
+    if cus:
+        monkeypatch.setenv("ACEHIP_ATTN_CUS", str(cus))
+    monkeypatch.setenv("ACEHIP_ATTN_PW", "2")
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(S + cus)
+    q = torch.randn(B, H, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    k = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    v = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    outs = {}
+    for pers in ("1", "0"):
+        monkeypatch.setenv("ACEHIP_ATTN_PERSIST", pers)
+        o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, S, S,
+                                                window, 1 / math.sqrt(128), ff.stream_ptr()))
+        torch.cuda.synchronize()
+        outs[pers] = o
+    ref = _attn_ref(q, k, v, window).transpose(1, 2).reshape(B, S, H * 128)
+    assert rel_l2(outs["1"].float().cpu(), ref.cpu()) < 1e-2
+    assert torch.equal(outs["1"], outs["0"])
+
+
 def _attn_ref(q, k, v, window):
     Sq, Sk = q.shape[2], k.shape[2]
     rep = q.shape[1] // k.shape[1]
