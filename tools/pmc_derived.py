@@ -2,7 +2,11 @@
 """Derived per-kernel MFMA figures from a SQ/GRBM counter pass and the kernel-trace
 stats of the same code (MI355X_MICROARCH.md 'DVFS give-back' and §rocprofv3):
   mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
-  clock_GHz      = (GRBM_GUI_ACTIVE / 8) / average kernel duration (trace stats)
+  clock_GHz      = (GRBM_GUI_ACTIVE / 8) / average kernel duration (trace stats), withheld
+                   (null, the raw quotient kept as clock_quotient_GHz) above the part's 2.4 GHz:
+                   the counter pass and the trace are different runs, and for short kernels
+                   the quotient is biased high (VERDICT r02 Weak 7); tools/pmc_roofline.py
+                   derives the roofline kernel's clock from its own pass per dispatch instead
   peak_at_clock  = 2.5 PF x clock / 2.4 GHz (bf16 dense)
 usage: pmc_derived.py PMC_SQ_JSON KERNEL_STATS_MD OUT_JSON"""
 import json
@@ -25,7 +29,9 @@ for k, v in pmc.items():
     us = avg.get(k)
     if us:
         clk = g / 8 / (us * 1e-6) / 1e9
-        row.update({"avg_us_trace": us, "clock_GHz": round(clk, 3), "peak_bf16_TFs_at_clock": round(2500 * clk / 2.4, 1)})
+        ok = clk <= 2.4
+        row.update({"avg_us_trace": us, "clock_quotient_GHz": round(clk, 3), "clock_GHz": round(clk, 3) if ok else None,
+                    "peak_bf16_TFs_at_clock": round(2500 * clk / 2.4, 1) if ok else None})
     out[k] = row
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, r in sorted(out.items(), key=lambda kv: -kv[1]["mfma_busy_frac"])[:20]:
