@@ -78,6 +78,7 @@ struct SplitArgs {
     float *ws;     // ≥ (units − full)·nsplit·8·66·64 floats
     int *cnt;      // ≥ units − full ints, zero between launches
     int units = 0; // attn_pw_kernel: > 0 = persistent over units [0, units) (no splits)
+    int dbg = 0;   // timing experiments only (ACEHIP_ATTN_DBG, wrong results): 1 = tail parts skip the hand-off
 };
 
 // ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
@@ -124,6 +125,104 @@ __device__ __forceinline__ void lgkm_wait8(bf16x8 (&f)[8]) {
 
 __device__ __forceinline__ int kvoff(int row, int ch) {
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+// Tail-split / short-split hand-off of one wave's (or pw sub-block's) partial (O, m, l):
+// 16 KB of O as sixteen 1-KB lane-contiguous chunks (chunk k = O[k / 4][4(k % 4) .. +3] of
+// every lane) + (m, l) per lane, published by write-through (sc1) 16-B stores and read back
+// by the last arriver with sc1 16-B loads: with the relaxed agent-scope ticket in between this
+// is a complete cross-XCD hand-off without a fence (cdna_hip_programming.md §5 "Projection GEMM
+// at M = 256" item 2).  Each is ONE asm statement — all loads in flight before the single
+// wait, and no register copy of a load's destination can sit between a load and its wait.
+__device__ __forceinline__ f32x4 sub4(const f32x16 &v, int q) {
+    return f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+__device__ __forceinline__ void slab_store(float *slab, const f32x16 (&o)[4], float m, float l, int lane) {
+    float *b0 = slab + lane * 4, *b1 = b0 + 4 * 256, *b2 = b0 + 8 * 256, *b3 = b0 + 12 * 256;
+    float *bm = slab + 16 * 256 + lane * 2;
+    const f32x2 ml = {m, l};
+    asm volatile(
+        "global_store_dwordx4 %0, %5, off sc1\n\t"
+        "global_store_dwordx4 %0, %6, off offset:1024 sc1\n\t"
+        "global_store_dwordx4 %0, %7, off offset:2048 sc1\n\t"
+        "global_store_dwordx4 %0, %8, off offset:3072 sc1\n\t"
+        "global_store_dwordx4 %1, %9, off sc1\n\t"
+        "global_store_dwordx4 %1, %10, off offset:1024 sc1\n\t"
+        "global_store_dwordx4 %1, %11, off offset:2048 sc1\n\t"
+        "global_store_dwordx4 %1, %12, off offset:3072 sc1\n\t"
+        "global_store_dwordx4 %2, %13, off sc1\n\t"
+        "global_store_dwordx4 %2, %14, off offset:1024 sc1\n\t"
+        "global_store_dwordx4 %2, %15, off offset:2048 sc1\n\t"
+        "global_store_dwordx4 %2, %16, off offset:3072 sc1\n\t"
+        "global_store_dwordx4 %3, %17, off sc1\n\t"
+        "global_store_dwordx4 %3, %18, off offset:1024 sc1\n\t"
+        "global_store_dwordx4 %3, %19, off offset:2048 sc1\n\t"
+        "global_store_dwordx4 %3, %20, off offset:3072 sc1\n\t"
+        "global_store_dwordx2 %4, %21, off sc1\n\t"
+        "s_nop 1"
+        :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(bm),
+           "v"(sub4(o[0], 0)), "v"(sub4(o[0], 1)), "v"(sub4(o[0], 2)), "v"(sub4(o[0], 3)),
+           "v"(sub4(o[1], 0)), "v"(sub4(o[1], 1)), "v"(sub4(o[1], 2)), "v"(sub4(o[1], 3)),
+           "v"(sub4(o[2], 0)), "v"(sub4(o[2], 1)), "v"(sub4(o[2], 2)), "v"(sub4(o[2], 3)),
+           "v"(sub4(o[3], 0)), "v"(sub4(o[3], 1)), "v"(sub4(o[3], 2)), "v"(sub4(o[3], 3)), "v"(ml)
+        : "memory");
+}
+__device__ __forceinline__ void slab_load(const float *slab, f32x16 (&o)[4], float &m, float &l, int lane) {
+    const float *b0 = slab + lane * 4, *b1 = b0 + 4 * 256, *b2 = b0 + 8 * 256, *b3 = b0 + 12 * 256;
+    const float *bm = slab + 16 * 256 + lane * 2;
+    f32x4 v[16];
+    f32x2 ml;
+    asm volatile(
+        "global_load_dwordx4 %0, %17, off sc1\n\t"
+        "global_load_dwordx4 %1, %17, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %17, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %17, off offset:3072 sc1\n\t"
+        "global_load_dwordx4 %4, %18, off sc1\n\t"
+        "global_load_dwordx4 %5, %18, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %6, %18, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %7, %18, off offset:3072 sc1\n\t"
+        "global_load_dwordx4 %8, %19, off sc1\n\t"
+        "global_load_dwordx4 %9, %19, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %10, %19, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %11, %19, off offset:3072 sc1\n\t"
+        "global_load_dwordx4 %12, %20, off sc1\n\t"
+        "global_load_dwordx4 %13, %20, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %14, %20, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %15, %20, off offset:3072 sc1\n\t"
+        "global_load_dwordx2 %16, %21, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+          "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]),
+          "=&v"(v[14]), "=&v"(v[15]), "=&v"(ml)
+        : "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(bm)
+        : "memory");
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[k >> 2][4 * (k & 3) + e] = v[k][e];
+    m = ml[0];
+    l = ml[1];
+}
+// fold part (o2, m2, l2) into the running merge (o, m, l) — the same expression for every
+// part whether it was loaded or is the last arriver's own, so the result does not depend on
+// which part arrived last (bit-reproducible)
+__device__ __forceinline__ void slab_fold(f32x16 (&o)[4], float &m, float &l, const f32x16 (&o2)[4], float m2,
+                                          float l2, bool first) {
+    if (first) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = o2[i];
+        m = m2;
+        l = l2;
+        return;
+    }
+    const float mn = fmaxf(m, m2);
+    const float a1 = __builtin_amdgcn_exp2f(m - mn), a2 = __builtin_amdgcn_exp2f(m2 - mn);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[i][j] = o[i][j] * a1 + o2[i][j] * a2;
+    l = l * a1 + l2 * a2;
+    m = mn;
 }
 
 // NREP = query heads per KV head handled by one workgroup (GQA sharing:
@@ -452,50 +551,32 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     }
     if (DEFER && pending) pv_slot(pend_slot, pf);
 
+    if (nsplit > 1 && (sp.dbg & 1)) return;
     if (nsplit > 1) {
-        // publish this part's (O, m, l) in lane order, then take a ticket; the last
-        // part merges the others (they published before their tickets) — no spinning.
-        // Agent-scope relaxed atomic stores/loads (sc1: coherent across the XCDs' L2s)
-        // plus vmcnt(0) order the hand-off; a __threadfence() would write back and
-        // invalidate the whole L2 and evict every co-resident workgroup's K/V tiles.
+        // publish this part's (O, m, l) (slab_store: write-through 16-B stores), then take a
+        // ticket; the last part merges every part in part order, its own from registers — no
+        // spinning, no fence (a __threadfence() would write back and invalidate the whole L2
+        // and evict every co-resident workgroup's K/V tiles)
         const int64_t wsz = 66 * 64;                   // floats per wave: 64 O + m + l per lane
-        float *mine = sp.ws + (((int64_t)(u - sp.full) * nsplit + part) * 8 + wave) * wsz;
-        auto st_c = [](float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-        auto ld_c = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) st_c(mine + (16 * i + j) * 64 + lane, oacc[i][j]);
-        st_c(mine + 64 * 64 + lane, m);
-        st_c(mine + 65 * 64 + lane, l);
+        float *const ws_u = sp.ws + (int64_t)(u - sp.full) * nsplit * 8 * wsz;
+        slab_store(ws_u + ((int64_t)part * 8 + wave) * wsz, oacc, m, l, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         __shared__ int s_ticket;
         if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
         __syncthreads();
         if (s_ticket != nsplit - 1) return;
-        // merge ALL parts (this one re-read too) in part order: the result does not depend on
-        // which part finished last (bit-reproducible from run to run)
+        const f32x16 own[4] = {oacc[0], oacc[1], oacc[2], oacc[3]};
+        const float m_own = m, l_own = l;
         for (int p2 = 0; p2 < nsplit; ++p2) {
-            const float *oth = sp.ws + (((int64_t)(u - sp.full) * nsplit + p2) * 8 + wave) * wsz;
-            const float m2 = ld_c(oth + 64 * 64 + lane), l2 = ld_c(oth + 65 * 64 + lane);
-            if (p2 == 0) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) oacc[i][j] = ld_c(oth + (16 * i + j) * 64 + lane);
-                l = l2;
-                m = m2;
-                continue;
+            if (p2 == part) {
+                slab_fold(oacc, m, l, own, m_own, l_own, p2 == 0);
+            } else {
+                f32x16 o2[4];
+                float m2, l2;
+                slab_load(ws_u + ((int64_t)p2 * 8 + wave) * wsz, o2, m2, l2, lane);
+                slab_fold(oacc, m, l, o2, m2, l2, p2 == 0);
             }
-            const float mn = fmaxf(m, m2);
-            const float a1 = __builtin_amdgcn_exp2f(m - mn), a2 = __builtin_amdgcn_exp2f(m2 - mn);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) oacc[i][j] = oacc[i][j] * a1 + ld_c(oth + (16 * i + j) * 64 + lane) * a2;
-            l = l * a1 + l2 * a2;
-            m = mn;
         }
         if (tid == 0) sp.cnt[u - sp.full] = 0;         // self-resetting for the next launch
     }
@@ -1083,8 +1164,12 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         oacc[i >> 6][(i >> 4) & 3][i & 15] = pw_oread<PW_O + i>();
     });
 
+    if (nsplit > 1 && (sp.dbg & 1)) return;
     if (nsplit > 1) {
-        // tail-split hand-off as in attn_fwd_kernel; "sub-wave" index 2·wave + sb
+        // tail-split hand-off as in attn_fwd_kernel's first version (4-B agent-scope relaxed
+        // atomics; pw runs split only off the production path): the 16-B slab form's register
+        // footprint beside both sub-blocks' O pushes hipcc past 256 arch VGPRs into AGPR
+        // spills, which this kernel's asm-owned AGPRs cannot take.  "sub-wave" index 2·wave + sb
         const int64_t wsz = 66 * 64;
         auto st_c = [](float *p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
         auto ld_c = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1226,6 +1311,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     if (grp == 2 && !kmask && window != ATTN_CAUSAL && (pw_mask & kind_bit)) {
         const int units = nq * KV * B;
         SplitArgs sp{nq, units, 1, nullptr, nullptr};
+        if (const char *e = getenv("ACEHIP_ATTN_DBG")) sp.dbg = atoi(e);
         const int tail = units % cus;
         int split_min = 24;        // shortest KV loop (tiles) whose tail units are split over KV ranges
         if (const char *e = getenv("ACEHIP_ATTN_PW_SPLIT")) split_min = atoi(e);
@@ -1259,6 +1345,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     const int nrep = split_heads ? 1 : grp;
     const int units = nq * KV * (grp / nrep) * B;
     SplitArgs sp{nq, units, 1, nullptr, nullptr};
+    if (const char *e = getenv("ACEHIP_ATTN_DBG")) sp.dbg = atoi(e);
     // one workgroup per CU: a partial last round of whole units is replaced by
     // tail units split over ⌊CUs / tail⌋ KV ranges (1.5 rounds instead of 2 at
     // 384 units on 256 CUs)
