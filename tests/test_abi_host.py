@@ -116,3 +116,40 @@ def test_lora_merge_state_dict():
     assert not any("lora" in k or "base_layer" in k for k in sd)
     q.disable_adapters = True
     assert torch.equal(merged_decoder_state_dict(m)["layers.0.self_attn.q_proj.weight"], q.base_layer.weight)
+
+
+def test_pw_kernel_agprs_stay_asm_owned(tmp_path):
+    """attn_pw_kernel owns a[0:255] by number from inline asm (O, Q and the K fragments live
+    there across the tile loop), so hipcc must never place a value of its own in an AGPR: a
+    VGPR spill into AGPRs (the compiler's first choice once arch VGPRs run out) would be
+    overwritten by the asm and corrupt addresses or results (seen once in round 3 as an
+    illegal address).  Compile the kernel to gfx950 assembly and require that every
+    v_accvgpr_read / v_accvgpr_write of the kernel body comes from an inline-asm block."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(REPO, "ace-step-1.5_amd", "csrc", "attention.hip")
+    out = tmp_path / "attention.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", src, "-o",
+                    str(out)], check=True, capture_output=True)
+    body, inside, in_asm, compiler_agpr = [], False, False, []
+    for line in out.read_text().splitlines():
+        if re.match(r"^_ZN6acehip12_GLOBAL__N_114attn_pw_kernel\S*:", line):
+            inside = True
+            continue
+        if not inside:
+            continue
+        if "s_endpgm" in line:
+            break
+        body.append(line)
+        if ";;#ASMSTART" in line:
+            in_asm = True
+        elif ";;#ASMEND" in line:
+            in_asm = False
+        elif not in_asm and re.search(r"v_accvgpr_(read|write)", line):
+            compiler_agpr.append(line.strip())
+    assert body, "attn_pw_kernel not found in the assembly"
+    assert not compiler_agpr, f"hipcc uses AGPRs in attn_pw_kernel: {compiler_agpr[:4]}"
+    assert not any("scratch_" in ln for ln in body), "attn_pw_kernel spills to scratch"
