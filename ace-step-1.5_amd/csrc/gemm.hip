@@ -1396,6 +1396,10 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 11: return launch_w4<192>(a, s);             // 4 waves, 96x128 wave tile, pipelined fragments
         case 12: return launch_pp<128>(a, s);             // ping-pong 128x256 (96 KiB), 64x64 wave tiles
         case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
+        // small-M A/B (tools/bench_small_m.py): narrow-N tiles so a whole-K grid reaches the chip
+        case 15: return launch<128, 64, 4, 1, 3>(a, s);   // 4 waves × 32 rows × 64 columns, 3-stage (72 KiB)
+        case 16: return launch<128, 64, 4, 1, 4>(a, s);   // same, 4-stage (96 KiB)
+        case 17: return launch<128, 64, 2, 1, 3>(a, s);   // 2 waves × 64 rows × 64 columns, 3-stage
         case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30: {
             // diagnostics / A/B: pp store, see gemm_pp_kernel DBG and SPL
             if (a.N % 256 || a.epi != EPI_STORE) return fail(-1, "gemm: diagnostic variant");
@@ -1550,13 +1554,25 @@ static int gemm_skinny(const GemmArgs &a, hipStream_t s, int depth = 0, RowAdd *
     return splitk_finish(a, a, splits, s);
 }
 
+// split-K tile width: 64-column tiles double the grid at a given split count (half the splits
+// and partial bytes for ~1 block per CU).  Measured at M = 125, cold weights, one process
+// (tools/bench_small_m.py, profiles/r03_small_m.log): down (N 2048, K 6144) 19.9 → 17.9 µs,
+// QKV (N 4096, K 2048) 18.8 → 17.2, but O (N 2048, K 2048: 4 K-tiles per split) 18.7 → 25.3 —
+// so 64 where N or K ≥ 4096.  ACEHIP_SPLITK_BN = 128 | 64 forces one (A/B; read per call)
+static int splitk_bn(const GemmArgs &a) {
+    const char *e = getenv("ACEHIP_SPLITK_BN");
+    if (e) return atoi(e) == 64 ? 64 : 128;
+    return (a.N >= 4096 || a.K >= 4096) ? 64 : 128;
+}
 static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s, RowAdd *defer = nullptr) {
     GemmArgs p = a;
     const int nk = a.K / BK;
     p.kper = (nk + splits - 1) / splits;
     splits = (nk + p.kper - 1) / p.kper;
-    const int tiles = ((a.M + 127) / 128) * (a.N / 128);
-    if (splitk_stages(a.N) == 3) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
+    const int bn = splitk_bn(a);
+    const int tiles = ((a.M + 127) / 128) * (a.N / bn);
+    if (bn == 64) gemm_kernel<128, 64, 4, 1, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
+    else if (splitk_stages(a.N) == 3) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     HIP_TRY(hipGetLastError());
     if (defer) {
@@ -1745,13 +1761,21 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
         const int rc = gemm_skinny(a, s, 0, dfr ? defer : nullptr);
         if (rc <= 0) return rc;   // done (0) or failed (< 0); 1 = workspace too small
     }
+    // SwiGLU of one 128-row chunk (turbo / short songs, M ≤ 128): whole-K 128×64 tiles with the
+    // SwiGLU epilogue fused (variant 16: no fp32 partials, no second launch) — M = 125, cold
+    // weights: 26.1 → 19.0 µs (tools/bench_small_m.py).  ACEHIP_SMALLM_WHOLEK=0: split-K (A/B)
+    if (a.epi == EPI_SWIGLU && a.M <= 128 && a.N % 64 == 0 && g_variant_override < 0) {
+        const char *e = getenv("ACEHIP_SMALLM_WHOLEK");
+        if (!(e && e[0] == '0')) return gemm_variant(a, 16, s);
+    }
     if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
         const int cus = num_cus();
         const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);
         const int nk = a.K / BK;
         if (tiles * 2 <= cus && nk >= 8) {
+            const int64_t tb = ((a.M + 127) / 128) * (a.N / splitk_bn(a));   // grid tiles of the split kernel
             int splits = (int)std::min<int64_t>(std::min<int64_t>(16, nk / splitk_min_ktiles()),
-                                                (splitk_fill() * cus + tiles - 1) / tiles);
+                                                (splitk_fill() * cus + tb - 1) / tb);
             const size_t need = (size_t)splits * a.M * a.N * 4 + (size_t)a.M * a.N * 2;
             if (splits >= 2 && need <= a.ws_bytes) return gemm_splitk(a, splits, s, dfr ? defer : nullptr);
         }

@@ -632,6 +632,44 @@ def test_forward_graph_replay_matches_eager(gpu_device):
     rt.close()
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(125, 12288, 2048, EPI_SWIGLU), (128, 12288, 2048, EPI_SWIGLU),
+                                       (77, 1024, 512, EPI_SWIGLU), (1, 12288, 2048, EPI_SWIGLU),
+                                       (125, 2048, 6144, EPI_RES), (125, 4096, 2048, EPI_STORE),
+                                       (250, 4096, 2048, EPI_STORE), (125, 2048, 2048, EPI_RES)])
+def test_gemm_small_m_paths(gpu_device, monkeypatch, M, N, K, epi):
+    """Turbo / short-song GEMMs (M ≤ 256): SwiGLU of one 128-row chunk on whole-K 128×64 tiles
+    with the epilogue fused (ACEHIP_SMALLM_WHOLEK), and the split-K path on 64- or 128-column
+    tiles (ACEHIP_SPLITK_BN, default 64 where N or K ≥ 4096): every variant vs fp32 torch."""
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(gpu_device, torch.bfloat16)
+    ncol = N // 2 if epi == EPI_SWIGLU else N
+    C0 = torch.randn(M, ncol, generator=g).to(gpu_device, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    if epi == EPI_SWIGLU:
+        y = ref.bfloat16().float().view(M, N // 64, 2, 32)
+        gate, up = y[:, :, 0, :].reshape(M, ncol), y[:, :, 1, :].reshape(M, ncol)
+        want, tol = torch.nn.functional.silu(gate).bfloat16().float() * up, 1e-2
+        knobs = [{"ACEHIP_SMALLM_WHOLEK": "1"}, {"ACEHIP_SMALLM_WHOLEK": "0"}]
+    else:
+        want, tol = ref + (C0.float() if epi == EPI_RES else 0), (1e-2 if epi == EPI_RES else 5e-3)
+        knobs = [{}, {"ACEHIP_SPLITK_BN": "64"}, {"ACEHIP_SPLITK_BN": "128"}]
+    for kn in knobs:
+        for k, v in kn.items():
+            monkeypatch.setenv(k, v)
+        C = C0.clone()
+        ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), ncol, M, N, K, None, epi, -1,
+                                              ff.stream_ptr()))
+        torch.cuda.synchronize()
+        assert torch.isfinite(C.float()).all(), kn
+        err = rel_l2(C.float().cpu(), want.cpu()) if epi != EPI_RES else \
+            rel_l2((C.float() - C0.float()).cpu(), ref.cpu())
+        assert err < tol, (kn, err)
+        for k in kn:
+            monkeypatch.delenv(k)
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(6000, 12288, 2048, EPI_SWIGLU), (15000, 12288, 2048, EPI_SWIGLU),
                                        (6000, 12288, 2048, EPI_STORE)])
 def test_gemm_tail_split(gpu_device, monkeypatch, M, N, K, epi):
