@@ -1280,6 +1280,16 @@ static int num_cus_attn() {
     return n;
 }
 
+// short-sequence KV split (a grid of a few units, e.g. the 10 s song's cross-attention: 8
+// units): KV tiles per part.  ACEHIP_ATTN_SHORT_TPP (A/B; read per call).  Turbo 10 s cross
+// (11 tiles, 8 units; tools/gpu_r03z.sh, one process): 1 tile per part 28.5 µs, 2: 22.7, 3: 20.3
+// (DiT song 27.7 / 27.1 / 26.8 ms) — fewer, longer parts pay fewer hand-offs; default 3
+static int short_tpp() {
+    const char *e = getenv("ACEHIP_ATTN_SHORT_TPP");
+    const int v = e ? atoi(e) : 3;
+    return v > 0 ? v : 3;
+}
+
 size_t attention_ws_bytes() {
     const size_t cus = std::max<size_t>(1024, (size_t)num_cus_attn());
     return cus * 8 * 66 * 64 * sizeof(float) + cus * sizeof(int);   // ≤ cus split parts in flight
@@ -1320,7 +1330,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
             sp.nsplit = min(4, cus / tail);
         } else if (ws && window < 0 && units * 2 <= cus && unit_tiles >= 4) {
             sp.full = 0;
-            sp.nsplit = min(min(cus / units, unit_tiles / 2), 16);
+            sp.nsplit = min(min(cus / units, (unit_tiles + short_tpp() - 1) / short_tpp()), 16);
         }
         if (sp.nsplit > 1) {
             sp.cnt = (int *)ws;
@@ -1364,7 +1374,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         // short sequences (a few query blocks): every unit split over KV ranges so the
         // grid reaches the CUs (cross-attention of a 10 s song: 8 units → 40 parts)
         sp.full = 0;
-        sp.nsplit = min(min(cus / units, unit_tiles / 2), 16);
+        sp.nsplit = min(min(cus / units, (unit_tiles + short_tpp() - 1) / short_tpp()), 16);
         sp.cnt = (int *)ws;
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
     }
