@@ -1301,6 +1301,10 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     if (B <= 0 || Sq <= 0) return 0;
     if (Sk <= 0 || KV <= 0 || H % KV) return fail(-1, "attention: bad heads/lengths");
     if (o_ld % 8) return fail(-1, "attention: o_ld must be a multiple of 8");
+    // a band wider than the sequence (|i − j| ≤ max(Sq, Sk) − 1 ≤ window: every pair admitted)
+    // is full attention — the 10 s songs' sliding layers (S = 125, window 128) then run the full
+    // kernel without per-tile band classification and masks
+    if (window >= 0 && !kmask && std::max(Sq, Sk) - 1 <= window) window = -1;
     const int grp = H / KV;
     const float sl2 = scale * 1.4426950408889634f;
     const int nq = (Sq + QB - 1) / QB;
