@@ -24,6 +24,8 @@
 //   * the production tiles are the ping-pong kernels (gemm_pp_kernel, 256×256
 //     and 192×256, two wave groups one barrier apart so MFMA and LDS traffic
 //     overlap on every SIMD), picked per shape by gemm_pick_variant.
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 #include "headpost.h"
 
@@ -32,6 +34,24 @@ namespace {
 
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
+
+// launch-attached timing events (gemm_ext_events): a hipEventRecord around a launch is its own
+// barrier packet — ≈ 5.6 µs of idle GPU before and after the timed kernel on this stack
+// (turbo timeline, tools/timeline.py) — while hipExtLaunchKernel stamps the dispatch itself
+struct ExtEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+thread_local ExtEvents g_ext_ev;
+template <typename... KArgs, typename... Args>
+inline void klaunch(void (*kern)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    if (g_ext_ev.stop) {
+        hipEvent_t st = g_ext_ev.start;
+        g_ext_ev.start = nullptr;
+        hipExtLaunchKernelGGL(kern, grid, block, 0, s, st, g_ext_ev.stop, 0, args...);
+    } else {
+        kern<<<grid, block, 0, s>>>(args...);
+    }
+}
 #ifndef W4_DMA_EVERY
 #define W4_DMA_EVERY 0     // 4-wave GEMM refill spacing in MFMAs (0: spread over half B)
 #endif
@@ -1014,7 +1034,7 @@ int launch_w4(const GemmArgs &a, hipStream_t s) {
         case EPI_STORE: gemm_w4_kernel<BM, BN, EPI_STORE><<<tiles, 256, 0, s>>>(a); break;
         case EPI_GATED_RES: gemm_w4_kernel<BM, BN, EPI_GATED_RES><<<tiles, 256, 0, s>>>(a); break;
         case EPI_RES: gemm_w4_kernel<BM, BN, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_SWIGLU: gemm_w4_kernel<BM, BN, EPI_SWIGLU><<<tiles, 256, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_w4_kernel<BM, BN, EPI_SWIGLU>, dim3(tiles), dim3(256), s, a); break;
         case EPI_HEADPOST:
             if constexpr (BM == 192 && (BN == 256 || BN == 128)) {
                 gemm_w4_kernel<BM, BN, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
@@ -1349,7 +1369,7 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE><<<tiles, 512, 0, s>>>(a); break;
         case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_SWIGLU: gemm_pp_kernel<BM, EPI_SWIGLU><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
         case EPI_HEADPOST:
             if constexpr (BM == 192 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
@@ -1371,7 +1391,7 @@ int launch(const GemmArgs &a, hipStream_t s) {
         case EPI_STORE: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_STORE><<<tiles, NT, 0, s>>>(a); break;
         case EPI_GATED_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_GATED_RES><<<tiles, NT, 0, s>>>(a); break;
         case EPI_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_RES><<<tiles, NT, 0, s>>>(a); break;
-        case EPI_SWIGLU: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_SWIGLU><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_kernel<BM, BN, WM, WN, STAGES, EPI_SWIGLU>, dim3(tiles), dim3(NT), s, a); break;
         default: return fail(-1, "gemm: bad epilogue for this variant");
     }
     HIP_TRY(hipGetLastError());
@@ -1420,6 +1440,13 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         }
         default: return fail(-1, "gemm: bad variant");
     }
+}
+
+bool gemm_ext_events(hipEvent_t start, hipEvent_t stop) {
+    const bool consumed = g_ext_ev.stop && !g_ext_ev.start;
+    g_ext_ev.start = start;
+    g_ext_ev.stop = stop;
+    return consumed;
 }
 
 static int g_variant_override = -1;

@@ -59,6 +59,11 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer = nullptr);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
 int gemm_small(const GemmArgs &a, int mode, hipStream_t s);        // small-M A/B (needs ws)
 int gemm_sk_forced(const GemmArgs &a, hipStream_t s);              // stream-K 256² tile (needs sk_*)
+// Launch-attached timing events for the next GEMM of this thread (the SwiGLU paths: ping-pong,
+// generic and four-wave tiles): its first launch takes `start`, every launch `stop` (the last
+// completion wins), by hipExtLaunchKernel — no separate event packets in the stream.
+// gemm_ext_events(nullptr, nullptr) disarms; it returns whether `start` was consumed.
+bool gemm_ext_events(hipEvent_t start, hipEvent_t stop);
 
 // --------------------------------------------------------------- small ops --
 // y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16
