@@ -71,6 +71,7 @@ struct acehip_dit {
     bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
+    bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
     // constant V row and their cross-O output the per-layer constant cnull[l]
@@ -265,12 +266,16 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
 
     h->tables = A((size_t)L * 6 * D);
     h->layers.resize(L);
+    // the layers' cross K/V projections side by side: set_condition runs them as ONE GEMM
+    // (N = L·2·kvd) instead of L small-M ones
+    h->wckv_all = A((size_t)L * 2 * kvd * D);
     for (int i = 0; i < L; ++i) {
         auto &ly = h->layers[i];
         ly.n_sa = A(D); ly.n_ca = A(D); ly.n_mlp = A(D);
         ly.wqkv = A((size_t)(qd + 2 * kvd) * D); ly.wo = A((size_t)D * qd);
         ly.qn = A(128); ly.kn = A(128); ly.cqn = A(128); ly.ckn = A(128);
-        ly.wcq = A((size_t)qd * D); ly.wckv = A((size_t)2 * kvd * D); ly.wco = A((size_t)D * qd);
+        ly.wcq = A((size_t)qd * D); ly.wckv = h->wckv_all ? h->wckv_all + (size_t)i * 2 * kvd * D : nullptr;
+        ly.wco = A((size_t)D * qd);
         ly.wgu = A((size_t)2 * F * D); ly.wdown = A((size_t)D * F);
         if (!ok) break;
         const std::string p = "layers." + std::to_string(i);
@@ -332,7 +337,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->h1 = A(Bc * D); h->temb = A(Bc * D); h->proj = A(Bc * 6 * D);
     h->mod = A((size_t)L * Bc * 6 * D); h->mod_out = A(Bc * 2 * D);
     h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
-    h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd);
+    h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)L);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->sk_part = (float *)A(SK_PART_BYTES / 2);
@@ -508,13 +513,17 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
     int rc = hgemm(h, g, s);
     if (rc) return rc;
     const size_t per = (size_t)Bc * kvd * Lenc;
+    // every layer's K/V projection in one GEMM: M = Bc·Lenc rows × N = L·2·kvd (turbo 10 s:
+    // 641 × 49152 — a full-chip grid, where L separate N = 2048 GEMMs were small-M split-K
+    // launches + their epilogues); the k-norm / head-major scatter stays per layer
+    const int64_t ldkv = (int64_t)h->L * 2 * kvd;
+    GemmArgs k{};
+    k.A = h->E; k.lda = D; k.W = h->wckv_all; k.ldw = D; k.C = h->KVtmp; k.ldc = ldkv;
+    k.M = M; k.N = (int)ldkv; k.K = D; k.epi = EPI_STORE;
+    if ((rc = hgemm(h, k, s))) return rc;
     for (int l = 0; l < h->L; ++l) {
-        GemmArgs k{};
-        k.A = h->E; k.lda = D; k.W = h->layers[l].wckv; k.ldw = D; k.C = h->KVtmp; k.ldc = 2 * kvd;
-        k.M = M; k.N = 2 * kvd; k.K = D; k.epi = EPI_STORE;
-        if ((rc = hgemm(h, k, s))) return rc;
         HeadPostArgs p{};
-        p.src = h->KVtmp; p.ld_src = 2 * kvd; p.B = Bc; p.S = Lenc;
+        p.src = h->KVtmp + (size_t)l * 2 * kvd; p.ld_src = ldkv; p.B = Bc; p.S = Lenc;
         p.nq = 0; p.nk = h->cfg.kv_heads; p.nv = h->cfg.kv_heads;
         p.kw = h->layers[l].ckn; p.k = h->Kc + l * per; p.v = h->Vc + l * per;
         p.S_dst = Lenc; p.eps = h->cfg.eps;
