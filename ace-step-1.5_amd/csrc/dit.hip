@@ -72,6 +72,7 @@ struct acehip_dit {
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
+    bf16_t *gemv_act = nullptr;        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
     // constant V row and their cross-O output the per-layer constant cnull[l]
@@ -339,6 +340,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)L);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
+    h->gemv_act = A((size_t)16 * D);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->sk_part = (float *)A(SK_PART_BYTES / 2);
     h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
@@ -726,9 +728,9 @@ static int timestep_mlps(acehip_dit *h, const bf16_t *const emb[2], int rows, bf
             RUN(gemv_small(emb[e] + (size_t)r0 * 256, 256, h->te_l1[e], h->te_b1[e], h1 + (size_t)r0 * D, D, n, D,
                            256, 0, s));
             RUN(gemv_small(h1 + (size_t)r0 * D, D, h->te_l2[e], h->te_b2[e], temb_e[e] + (size_t)r0 * D, D, n, D, D,
-                           1, s));
+                           1, s, h->gemv_act));
             RUN(gemv_small(temb_e[e] + (size_t)r0 * D, D, h->te_tp[e], h->te_btp[e], proj_e[e] + (size_t)r0 * 6 * D,
-                           6 * D, n, 6 * D, D, 1, s));
+                           6 * D, n, 6 * D, D, 1, s, h->gemv_act));
         }
     }
     RUN(add_bf16(temb_e[0], temb_e[1], temb, (int64_t)rows * D, s));

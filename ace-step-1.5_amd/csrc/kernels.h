@@ -67,8 +67,9 @@ bool gemm_ext_events(hipEvent_t start, hipEvent_t stop);
 
 // --------------------------------------------------------------- small ops --
 // y[m][n] = bf16(Σ_k act(x[m][k])·W[n][k] + b[n]); act: 0 none, 1 bf16(silu(x)); M ≤ 16
+// act_scratch (≥ M·K elements): with act, bf16(silu(x)) is formed there once first
 int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
-               int64_t ldy, int M, int N, int K, int act, hipStream_t s);
+               int64_t ldy, int M, int N, int K, int act, hipStream_t s, bf16_t *act_scratch = nullptr);
 // sinusoid of bf16(t*1000): emb[b][0:128]=cos, [128:256]=sin, as bf16 (base:225-246)
 // dst[r][0..n) = src[0..n) for r < rows (n % 8 == 0)
 int bcast_rows(const bf16_t *src, int64_t n, bf16_t *dst, int rows, hipStream_t s);

@@ -22,9 +22,17 @@ __global__ __launch_bounds__(256) void gemv_small_kernel(const bf16_t *__restric
 #pragma unroll
     for (int m = 0; m < 16; ++m) acc[m] = 0.f;
     const bf16_t *wr = W + (int64_t)n * K;
-    for (int k = lane * 8; k < K; k += 512) {
+    // the row's W chunks (K ≤ 2048: ≤ 4 per lane) are all issued before the first FMA: the
+    // kernel is a latency chain per wave otherwise (one W round trip per 512 columns)
+    uint4 wq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = lane * 8 + c * 512;
+        if (k < K) wq[c] = *(const uint4 *)(wr + k);
+    }
+    for (int c = 0, k = lane * 8; k < K; ++c, k += 512) {
         float wv[8];
-        unpack8(*(const uint4 *)(wr + k), wv);
+        unpack8(c < 4 ? wq[c & 3] : *(const uint4 *)(wr + k), wv);
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
             if (m < M) {
@@ -46,6 +54,19 @@ __global__ __launch_bounds__(256) void gemv_small_kernel(const bf16_t *__restric
             if (lane == 0) y[m * ldy + n] = f2bf(v + bb);
         }
     }
+}
+
+// y = bf16(silu(x)) for the M ≤ 16 rows of a timestep-MLP input, once (gemv_small's act
+// operand; in-kernel it was recomputed for every output column: N·M·K transcendentals)
+__global__ __launch_bounds__(256) void silu_rows_kernel(const bf16_t *__restrict__ x, int64_t ldx,
+                                                        bf16_t *__restrict__ y, int64_t ldy, int K) {
+    const int m = blockIdx.y, k = (blockIdx.x * 256 + threadIdx.x) * 8;
+    if (k >= K) return;
+    float v[8];
+    unpack8(*(const uint4 *)(x + m * ldx + k), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = silu_f(v[j]);
+    *(uint4 *)(y + m * ldy + k) = pack8(v);
 }
 
 // dst row r (r = blockIdx.y) = src, 16 B per lane
@@ -274,8 +295,16 @@ int copy_cols(const bf16_t *src, int64_t lds, bf16_t *dst, int64_t ldd, int M, i
 }
 
 int gemv_small(const bf16_t *x, int64_t ldx, const bf16_t *W, const bf16_t *bias, bf16_t *y,
-               int64_t ldy, int M, int N, int K, int act, hipStream_t s) {
+               int64_t ldy, int M, int N, int K, int act, hipStream_t s, bf16_t *act_scratch) {
     if (M > 16 || K % 8 || ldx % 8) return fail(-1, "gemv_small: M<=16, K%8==0 required");
+    if (act && act_scratch && M > 0) {
+        // bf16(silu(x)) once into the scratch rows (same rounding as the in-kernel rbf(silu))
+        silu_rows_kernel<<<dim3((unsigned)((K / 8 + 255) / 256), M), 256, 0, s>>>(x, ldx, act_scratch, K, K);
+        HIP_TRY(hipGetLastError());
+        x = act_scratch;
+        ldx = K;
+        act = 0;
+    }
     gemv_small_kernel<<<(N + 3) / 4, 256, 0, s>>>(x, ldx, W, bias, y, ldy, M, N, K, act);
     HIP_TRY(hipGetLastError());
     return 0;
