@@ -131,6 +131,14 @@ class TextEncoderOutput:
         self.last_hidden_state = last_hidden_state
 
 
+def await_ready(t: Optional[torch.Tensor]) -> None:
+    """Make the current stream wait for a tensor that an overlapped ``TextEncoder`` is still
+    producing on its side stream (``_acehip_ready``, set by ``TextEncoder(overlap=True)``)."""
+    ev = getattr(t, "_acehip_ready", None)
+    if ev is not None:
+        torch.cuda.current_stream(t.device).wait_event(ev)
+
+
 class TextEncoder:
     """Qwen3-Embedding-0.6B (``Qwen3Model``) drop-in for the reference's ``text_encoder``
     (loaded at ``init_service_loader.py:146-160``, called by ``infer_text_embeddings`` /
@@ -144,12 +152,19 @@ class TextEncoder:
     QWEN3_06B = dict(hidden_size=1024, intermediate_size=3072, num_hidden_layers=28, num_attention_heads=16,
                      num_key_value_heads=8, head_dim=128, rms_norm_eps=1e-6, rope_theta=1_000_000.0)
 
-    def __init__(self, cfg: Optional[DiTConfig] = None, device: int = 0, max_batch: int = 8, max_tokens: int = 512):
+    def __init__(self, cfg: Optional[DiTConfig] = None, device: int = 0, max_batch: int = 8, max_tokens: int = 512,
+                 overlap: bool = False):
         self.cfg = cfg or DiTConfig(**self.QWEN3_06B)
         self.device = torch.device("cuda", device)
         self.stack = EncoderStack(self.cfg, self.cfg.num_hidden_layers, 0, device=device,
                                   max_tokens=max_batch * max_tokens, max_S=max_tokens, causal=True)
         self.embed_tokens: Optional[_EmbedTokens] = None
+        # overlap=True: the 28 layers run on a side stream and the call returns at once; the
+        # output carries the side stream's completion event (``_acehip_ready``), which the
+        # condition encoder waits for only after its lyric and timbre encoders are queued, so
+        # the independent encoder chains overlap.  Opt-in: a consumer that is not acehip's
+        # must call ``await_ready(last_hidden_state)`` before touching the tensor.
+        self._side = torch.cuda.Stream(self.device) if overlap else None
 
     @classmethod
     def from_reference_model(cls, model, **kw) -> "TextEncoder":
@@ -174,8 +189,19 @@ class TextEncoder:
                  **kwargs) -> TextEncoderOutput:
         if attention_mask is not None:
             raise NotImplementedError("TextEncoder: padding masks are not supported (the reference passes none)")
-        h = self.embed_tokens(input_ids)
-        return TextEncoderOutput(self.stack.forward(h))
+        if self._side is None:
+            h = self.embed_tokens(input_ids)
+            return TextEncoderOutput(self.stack.forward(h))
+        main = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(main)                 # input ids (and the weights) ready
+        with torch.cuda.stream(self._side):
+            h = self.embed_tokens(input_ids)
+            out = self.stack.forward(h)
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        out.record_stream(main)                      # read on the consumer's stream later
+        out._acehip_ready = ev
+        return TextEncoderOutput(out)
 
     def to(self, *a, **k) -> "TextEncoder":
         """The handler's offload context moves models with ``.to``; the handle stays resident."""
@@ -294,9 +320,12 @@ class ConditionEncoder:
     def __call__(self, text_hidden_states, text_attention_mask, lyric_hidden_states, lyric_attention_mask,
                  refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask):
         dev = self.device
-        text = self.text_projector(text_hidden_states)
+        # lyric and timbre first: an overlapped text encoder (TextEncoder(overlap=True)) is
+        # waited for only after them (the three chains are independent; results unchanged)
         lyric = self.lyric_encoder(lyric_hidden_states, lyric_attention_mask)
         timbre, timbre_mask = self.timbre_encoder(refer_audio_acoustic_hidden_states_packed, refer_audio_order_mask)
+        await_ready(text_hidden_states)
+        text = self.text_projector(text_hidden_states)
         enc, mask = pack_sequences(lyric, timbre, lyric_attention_mask.to(dev), timbre_mask)
         return pack_sequences(enc, text, mask, text_attention_mask.to(dev))
 
@@ -460,6 +489,7 @@ class HipPrepareCondition:
             precomputed_lm_hints_25Hz = self.detokenizer(q).to(hidden_states.dtype)
             need_tokenizer = False
         if need_tokenizer:
+            await_ready(text_hidden_states)          # the reference's code reads it at once
             if self.fallback is None:
                 raise NotImplementedError("acehip: cover conditioning needs the FSQ audio tokenizer "
                                           "(pass precomputed_lm_hints_25Hz or a reference fallback)")

@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--lyric-len", type=int, default=512)
     p.add_argument("--turbo", action="store_true",
                    help="turbo sampler (table schedule, no CFG; SURVEY config 1 shape: --seconds 10 --infer-steps 8)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="text encoder on the song's stream (default: on a side stream, overlapping the "
+                        "lyric / timbre encoders; the DiT starts only after all three)")
     p.add_argument("--repaint", action="store_true",
                    help="SURVEY config 5: VAE encode of a synthetic 48 kHz stereo source -> DiT repaint of "
                         "[--repaint-start, --repaint-end) s -> VAE decode, all inside the timed song")
@@ -256,7 +259,7 @@ def main():
         # the Qwen3-Embedding-0.6B text encoder (infer_text_embeddings / infer_lyric_embeddings,
         # conditioning_embed.py:71-79): 28 causal layers for the text tokens, the table for lyrics
         te_cfg = DiTConfig(**TextEncoder.QWEN3_06B)
-        te = TextEncoder(te_cfg, local, max_batch=1, max_tokens=max(args.text_len, 64))
+        te = TextEncoder(te_cfg, local, max_batch=1, max_tokens=max(args.text_len, 64), overlap=not args.no_overlap)
         te.load(synth_text_encoder_weights(te_cfg, QWEN3_VOCAB, seed=0, mode="bench", device=dev,
                                            dtype=torch.bfloat16, backend="torch"))
     be = AceStepDiTBackend(rt, null, is_turbo=args.turbo, prepare_condition=prep)

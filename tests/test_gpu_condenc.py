@@ -242,3 +242,33 @@ def test_prepare_condition_cover(gpu_device):
     assert torch.equal(ctx[1, :, :64], src[1])
     assert torch.equal(ctx[:, :, 64:], cm)
     ce.close(); tok.close(); det.close()
+
+
+def test_overlapped_text_encoder_feeds_condition_encoder(gpu_device):
+    """TextEncoder(overlap=True) runs its layers on a side stream and returns at once; the
+    condition encoder queues its lyric and timbre encoders first and waits for the text
+    encoder's event only before the text projector.  Same encoder states, bit for bit, as the
+    synchronous text encoder (real text width, 3 Qwen3 layers)."""
+    from acehip.condition import TextEncoder, await_ready
+    from acehip.weights import synth_text_encoder_weights
+    cfg, g, ce = _setup("full_bfloat16", gpu_device)
+    d = gpu_device
+    B, Lt = g["text"].shape[0], g["text"].shape[1]
+    te_cfg = DiTConfig(**dict(TextEncoder.QWEN3_06B, num_hidden_layers=3))
+    assert te_cfg.hidden_size == g["text"].shape[2]
+    W = {k: v.to(d) for k, v in synth_text_encoder_weights(te_cfg, 300, seed=5, mode="parity").items()}
+    ids = torch.randint(0, 300, (B, Lt), generator=torch.Generator().manual_seed(3)).to(d)
+    outs = {}
+    for ov in (False, True):
+        te = TextEncoder(te_cfg, device=d.index or 0, max_batch=B, max_tokens=max(Lt, 64), overlap=ov)
+        te.load(W)
+        text = te(input_ids=ids).last_hidden_state
+        enc, mask = ce(text, g["text_mask"].to(d), g["lyric"].to(d), g["lyric_mask"].to(d), g["refer"].to(d),
+                       g["order"].to(d))
+        await_ready(text)
+        torch.cuda.synchronize()
+        outs[ov] = (text.clone(), enc.clone(), mask.clone())
+        te.close()
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+    ce.close()

@@ -14,6 +14,12 @@ M = int(os.environ.get("M", "125"))
 # name: (N, K, epi)  epi 0 store, 2 residual (C += A·Wᵀ), 3 SwiGLU (C[M][N/2])
 shapes = {"swiglu": (12288, 2048, 3), "down": (2048, 6144, 2), "qkv": (4096, 2048, 0), "o": (2048, 2048, 2)}
 cases = {"prod": (-1, {}), "bn64": (-1, {"ACEHIP_SPLITK_BN": "64"}), "v15": (15, {}), "v16": (16, {}), "v17": (17, {})}
+if os.environ.get("SHAPES"):
+    shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
+if os.environ.get("CASES"):        # extra env cases: "name:K=V+K=V;name2:K=V"
+    for item in os.environ["CASES"].split(";"):
+        nm, kv = item.split(":")
+        cases[nm] = (-1, dict(x.split("=") for x in kv.split("+")))
 out = {}
 for name, (N, K, epi) in shapes.items():
     g = torch.Generator(device=dev).manual_seed(0)
