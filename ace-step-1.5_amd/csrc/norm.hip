@@ -56,6 +56,20 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *x,   // 
 #pragma unroll
         for (int i = 0; i < NV; ++i) xr[r][i] = *(const vec_t *)(xp + (i * 64 + lane) * V);
     }
+    // weight / modulation loads are independent of the row-add and the reductions: issued with
+    // the x loads, before any store of the row add (vmcnt also counts stores, so a load issued
+    // after them would make its wait cover their completion too)
+    vec_t wr[NV], s1r[NV], s2r[NV];
+    int cur_b = row0 / rows_per_batch;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int e = (i * 64 + lane) * V;
+        wr[i] = *(const vec_t *)(w + e);
+        if (scale) {
+            s1r[i] = *(const vec_t *)(scale + (int64_t)cur_b * mod_bstride + e);
+            s2r[i] = *(const vec_t *)(shift + (int64_t)cur_b * mod_bstride + e);
+        }
+    }
     // rows < ra.prows first get the deferred split-K residual epilogue of the GEMM that
     // produced them (gemm(..., defer)): x = bf16(x + bf16(bf16(Σ partials)·gate)) or
     // bf16(x + bf16(Σ partials)), summed in split order as splitk_epilogue_kernel does
@@ -110,18 +124,6 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(const bf16_t *x,   // 
                 xr[r][i] = packv<V>(xv);
                 *(vec_t *)(ra.xw + (int64_t)row * D + e) = xr[r][i];
             }
-        }
-    }
-    // weight / modulation loads are independent of the reductions: issue them first
-    vec_t wr[NV], s1r[NV], s2r[NV];
-    int cur_b = row0 / rows_per_batch;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const int e = (i * 64 + lane) * V;
-        wr[i] = *(const vec_t *)(w + e);
-        if (scale) {
-            s1r[i] = *(const vec_t *)(scale + (int64_t)cur_b * mod_bstride + e);
-            s2r[i] = *(const vec_t *)(shift + (int64_t)cur_b * mod_bstride + e);
         }
     }
     float rs[R];
@@ -198,6 +200,16 @@ __global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *x,   /
     uint4 xr[NV], wr[NV], s1r[NV], s2r[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) xr[i] = *(const uint4 *)(xp + ((wp * NV + i) * 64 + lane) * 8);
+    // weight / modulation vectors with the x loads, before the row add's stores (see rmsnorm_mod_kernel)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int e = ((wp * NV + i) * 64 + lane) * 8;
+        wr[i] = *(const uint4 *)(w + e);
+        if (scale) {
+            s1r[i] = *(const uint4 *)(scale + (int64_t)b * mod_bstride + e);
+            s2r[i] = *(const uint4 *)(shift + (int64_t)b * mod_bstride + e);
+        }
+    }
     if (ra.part && row < ra.prows) {               // wave-uniform
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
@@ -229,15 +241,6 @@ __global__ __launch_bounds__(256) void rmsnorm_split_kernel(const bf16_t *x,   /
             for (int j = 0; j < 8; ++j) xv[j] += av[j];
             xr[i] = pack8(xv);
             if (live) *(uint4 *)(ra.xw + (int64_t)row * D + e) = xr[i];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const int e = ((wp * NV + i) * 64 + lane) * 8;
-        wr[i] = *(const uint4 *)(w + e);
-        if (scale) {
-            s1r[i] = *(const uint4 *)(scale + (int64_t)b * mod_bstride + e);
-            s2r[i] = *(const uint4 *)(shift + (int64_t)b * mod_bstride + e);
         }
     }
     // lane L's running sum of squares continues across the row's waves in element order
