@@ -1283,7 +1283,9 @@ static int num_cus_attn() {
 // short-sequence KV split (a grid of a few units, e.g. the 10 s song's cross-attention: 8
 // units): KV tiles per part.  ACEHIP_ATTN_SHORT_TPP (A/B; read per call).  Turbo 10 s cross
 // (11 tiles, 8 units; tools/gpu_r03z.sh, one process): 1 tile per part 28.5 µs, 2: 22.7, 3: 20.3
-// (DiT song 27.7 / 27.1 / 26.8 ms) — fewer, longer parts pay fewer hand-offs; default 3
+// (DiT song 27.7 / 27.1 / 26.8 ms) — fewer, longer parts pay fewer hand-offs; 4 and 6 tiles
+// (after the slab hand-off, tools/gpu_r03m2.sh): 19.6 / 21.9 vs 19.7 µs, song 25.7 / 26.1 vs 25.6
+// ms; default 3
 static int short_tpp() {
     const char *e = getenv("ACEHIP_ATTN_SHORT_TPP");
     const int v = e ? atoi(e) : 3;
