@@ -204,6 +204,35 @@ def test_dit_forward_vs_reference_golden(gpu_device, name):
     rt.close()
 
 
+@pytest.mark.parametrize("name", ["full2_bfloat16", "full2_long_bfloat16"])
+def test_profile_events_do_not_change_results(gpu_device, name):
+    """acehip_dit_profile: the SwiGLU GEMM's timing events ride on its launches
+    (hipExtLaunchKernel start / stop, gemm_ext_events) and the other kinds are bracketed by
+    event records — every kind reports one launch per layer with a positive time, and the
+    forward is bit-identical with and without profiling (small-M whole-K and larger-M paths)."""
+    meta = golden_manifest()["forward"][name]
+    cfg = DiTConfig(**meta["cfg"])
+    g = load_golden("dit_fwd_" + name)
+    W = synth_dit_weights(cfg, seed=meta["seed"], mode="parity")
+    rt = _runtime(cfg, W, gpu_device, max_S=max(64, (meta["T"] + 1) // 2), max_Lenc=max(32, meta["Lenc"]))
+    rt.set_condition(g["enc"].to(gpu_device))
+    args = (g["xt"].to(gpu_device).contiguous(), g["ctx"].to(gpu_device).contiguous(),
+            g["t"].float().to(gpu_device), g["t_r"].float().to(gpu_device))
+    plain = rt.forward(*args).clone()
+    for kinds in (["gemm_swiglu"], None):
+        rt.profile(True, kinds=kinds)
+        prof = rt.forward(*args).clone()
+        torch.cuda.synchronize()
+        stats = rt.profile_read()
+        rt.profile(False)
+        assert torch.equal(plain, prof)
+        n, ms = stats["gemm_swiglu"]
+        assert n == cfg.num_hidden_layers and ms > 0, stats
+        if kinds is None:
+            assert stats["gemm_qkv"][0] == cfg.num_hidden_layers and stats["gemm_qkv"][1] > 0
+    rt.close()
+
+
 def test_dit_forward_cfg_rows_and_long_sequence(gpu_device):
     """Bx < Bc (CFG reads xt row b % Bx), odd T, band + full layers at S > 2·window,
     Lenc not a multiple of 64 — vs the bf16 CPU oracle."""
