@@ -134,15 +134,19 @@ def test_pw_kernel_agprs_stay_asm_owned(tmp_path):
     out = tmp_path / "attention.s"
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", src, "-o",
                     str(out)], check=True, capture_output=True)
-    body, inside, in_asm, compiler_agpr = [], False, False, []
+    # every instantiation (the band / full kernel and the SHIFT variant), each up to its
+    # .Lfunc_end label (early returns put several s_endpgm in one body)
+    bodies, body, in_asm, compiler_agpr = {}, None, False, []
     for line in out.read_text().splitlines():
-        if re.match(r"^_ZN6acehip12_GLOBAL__N_114attn_pw_kernel\S*:", line):
-            inside = True
+        mk = re.match(r"^(_ZN6acehip12_GLOBAL__N_114attn_pw_kernel\S*):", line)
+        if mk:
+            body = bodies.setdefault(mk.group(1), [])
             continue
-        if not inside:
+        if body is None:
             continue
-        if "s_endpgm" in line:
-            break
+        if line.startswith(".Lfunc_end"):
+            body = None
+            continue
         body.append(line)
         if ";;#ASMSTART" in line:
             in_asm = True
@@ -150,6 +154,7 @@ def test_pw_kernel_agprs_stay_asm_owned(tmp_path):
             in_asm = False
         elif not in_asm and re.search(r"v_accvgpr_(read|write)", line):
             compiler_agpr.append(line.strip())
-    assert body, "attn_pw_kernel not found in the assembly"
+    assert len(bodies) >= 2, f"attn_pw_kernel instantiations not found in the assembly: {list(bodies)}"
     assert not compiler_agpr, f"hipcc uses AGPRs in attn_pw_kernel: {compiler_agpr[:4]}"
-    assert not any("scratch_" in ln for ln in body), "attn_pw_kernel spills to scratch"
+    for name, b in bodies.items():
+        assert not any("scratch_" in ln for ln in b), f"{name} spills to scratch"

@@ -132,6 +132,35 @@ def test_attention_band_persistent(gpu_device, monkeypatch, cus, B, H, KV, S, wi
     assert torch.equal(outs["1"], outs["0"])
 
 
+@pytest.mark.parametrize("B,H,KV,S,window", [(2, 4, 2, 1000, 128), (1, 16, 8, 777, 64), (1, 2, 1, 450, 200),
+                                          (2, 4, 2, 333, 65), (1, 4, 2, 130, 127), (2, 16, 8, 3000, 128),
+                                          (1, 2, 1, 200, 64)])
+def test_attention_band_shift(gpu_device, monkeypatch, B, H, KV, S, window):
+    """ACEHIP_ATTN_SHIFT=1: each wave of attn_pw_kernel walks its own band tiles (odd waves one
+    tile ahead in a 4-slot ring) instead of the workgroup's union.  Same tiles per row in the same
+    order as the union walk (whose extra tiles a wave skips), so bit-identical to it; windows
+    that are / are not multiples of KT, ragged S with a partial last tile, a band touching both
+    sequence ends."""
+    monkeypatch.setenv("ACEHIP_ATTN_PW", "2")
+    monkeypatch.setenv("ACEHIP_ATTN_PERSIST", "0")
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(S + window)
+    q = torch.randn(B, H, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    k = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    v = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
+    outs = {}
+    for shift in ("1", "0"):
+        monkeypatch.setenv("ACEHIP_ATTN_SHIFT", shift)
+        o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, S, S,
+                                                window, 1 / math.sqrt(128), ff.stream_ptr()))
+        torch.cuda.synchronize()
+        outs[shift] = o
+    ref = _attn_ref(q, k, v, window).transpose(1, 2).reshape(B, S, H * 128)
+    assert rel_l2(outs["1"].float().cpu(), ref.cpu()) < 1e-2
+    assert torch.equal(outs["1"], outs["0"])
+
+
 def _attn_ref(q, k, v, window):
     Sq, Sk = q.shape[2], k.shape[2]
     rep = q.shape[1] // k.shape[1]
