@@ -72,7 +72,8 @@ struct acehip_dit {
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
-    bf16_t *gemv_act = nullptr;        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
+    bf16_t *gemv_act = nullptr;
+    float *gatef = nullptr;            // D: the fp32 AdaLN gate row of a hipBLASLt projection (ACEHIP_BLASLT)        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
     // constant V row and their cross-O output the per-layer constant cnull[l]
@@ -341,6 +342,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)L);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->gemv_act = A((size_t)16 * D);
+    h->gatef = (float *)A((size_t)2 * D);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->sk_part = (float *)A(SK_PART_BYTES / 2);
     h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
@@ -687,6 +689,9 @@ static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, 
                             knob_hash()};
         if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
             if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
+            // ACEHIP_BLASLT: one eager pass first, so the hipBLASLt handle, workspace, plans and
+            // code objects exist before the capture (the graph then replays the same body)
+            if (blaslt_mask()) RUN(forward_body(h, Bc, S, dup, ts_cached, s));
             if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
             HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
             const int brc = forward_body(h, Bc, S, dup, ts_cached, h->cap_stream);
@@ -764,6 +769,18 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // it (gemm sets pend.part only when it deferred).  Deferral needs that norm to cover every
     // row the GEMM wrote, and no X copy in between (the layer-0 CFG dedup).
     RowAdd pend{};
+    // ACEHIP_BLASLT (A/B, blaslt.hip): hipBLASLt for the large-M projections — QKV (bit 1: into
+    // Hb, free between the down projection and the next SwiGLU, + the standalone head_post),
+    // self-O / down (bit 2: gate as the α vector, needs one gate row for every batch row:
+    // the schedule's broadcast timestep), cross-O (bit 4).  blaslt_gemm returning 1 (no plan)
+    // falls through to the hand-written kernel.
+    const int ltm = blaslt_mask();
+    const bool gate_uniform = ts_cached || Bc == 1;
+    auto lt_gated = [&](const bf16_t *Aop, int64_t lda, const bf16_t *Wop, int rows, int K, const bf16_t *gate) {
+        int rc2 = gate_to_f32(gate, h->gatef, D, s);
+        if (rc2) return rc2;
+        return blaslt_gemm(Aop, lda, Wop, K, h->X, D, rows, D, K, h->gatef, 1.0f, s);
+    };
     for (int l = 0; l < L; ++l) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
@@ -779,7 +796,19 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         q.hp.B = Bs; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
-        RUN(timed(h, 2, s, [&] { return hgemm(h, q, s); }));
+        RUN(timed(h, 2, s, [&] {
+            if ((ltm & 1) && Ms > 256 && (size_t)F >= (size_t)q.N) {
+                const int r2 = blaslt_gemm(h->XN, D, ly.wqkv, D, h->Hb, q.N, Ms, q.N, D, nullptr, 0.0f, s);
+                if (r2 <= 0) {
+                    if (r2 < 0) return r2;
+                    HeadPostArgs hh = q.hp;
+                    hh.src = h->Hb;
+                    hh.ld_src = q.N;
+                    return head_post(hh, s);
+                }
+            }
+            return hgemm(h, q, s);
+        }));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
             return attention(h->Qh, h->Kh, h->Vh, h->AO, Bs, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
                              scale, qd, h->attn_ws, s);
@@ -789,7 +818,13 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         o.M = Ms; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
         const bool defer_o = fuse_rowadd && Bs == Bc && (Mq == M || Mq == 0);
-        RUN(timed(h, 3, s, [&] { return hgemm(h, o, s, defer_o ? &pend : nullptr); }));
+        RUN(timed(h, 3, s, [&] {
+            if ((ltm & 2) && Ms > 256 && gate_uniform) {
+                const int r2 = lt_gated(h->AO, qd, ly.wo, Ms, qd, md + 2 * D);
+                if (r2 <= 0) return r2;
+            }
+            return hgemm(h, o, s, defer_o ? &pend : nullptr);
+        }));
         for (int b = Bs; b < Bc; ++b)
             HIP_TRY(hipMemcpyAsync(h->X + (size_t)b * S * D, h->X, (size_t)S * D * 2, hipMemcpyDeviceToDevice, s));
         // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
@@ -810,7 +845,13 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
             GemmArgs co{};
             co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
             co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
-            RUN(timed(h, 3, s, [&] { return hgemm(h, co, s, fuse_rowadd ? &pend : nullptr); }));
+            RUN(timed(h, 3, s, [&] {
+                if ((ltm & 4) && Mq > 256) {
+                    const int r2 = blaslt_gemm(h->AO, qd, ly.wco, qd, h->X, D, Mq, D, qd, nullptr, 1.0f, s);
+                    if (r2 <= 0) return r2;
+                }
+                return hgemm(h, co, s, fuse_rowadd ? &pend : nullptr);
+            }));
         }
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533); the null rows' constant cross-O output
         // is added inside the norm pass (ACEHIP_FUSE_ROWADD=0: separate add_row_bcast, A/B)
@@ -834,7 +875,13 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
-        RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr); }));
+        RUN(timed(h, 1, s, [&] {
+            if ((ltm & 2) && M > 256 && gate_uniform) {
+                const int r2 = lt_gated(h->Hb, F, ly.wdown, M, F, md + 5 * D);
+                if (r2 <= 0) return r2;
+            }
+            return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr);
+        }));
     }
     // norm_out AdaLN (base:1491-1497); proj_out runs after the body
     RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s, pend));

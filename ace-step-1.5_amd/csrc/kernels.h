@@ -119,6 +119,11 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
                 hipStream_t s, RowAdd ra = RowAdd{}, int rows_per_wave = 0);
 int head_post(const HeadPostArgs &a, hipStream_t s);
+// hipBLASLt alternative for the N <= 4096 projections (blaslt.hip; ACEHIP_BLASLT bit mask)
+int blaslt_mask();
+int blaslt_gemm(const bf16_t *A, int64_t lda, const bf16_t *W, int64_t ldw, bf16_t *C, int64_t ldc, int M, int N,
+                int K, const float *alpha_vec, float beta, hipStream_t s);
+int gate_to_f32(const bf16_t *g, float *o, int n, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---
 // ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials
