@@ -116,16 +116,4 @@ int blaslt_gemm(const bf16_t *A, int64_t lda, const bf16_t *W, int64_t ldw, bf16
     return 0;
 }
 
-__global__ void gate_f32_kernel(const bf16_t *__restrict__ g, float *__restrict__ o, int n) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) o[i] = bf2f(g[i]);
-}
-
-// the AdaLN gate row (bf16, as the reference rounds it) as the fp32 α vector of blaslt_gemm
-int gate_to_f32(const bf16_t *g, float *o, int n, hipStream_t s) {
-    gate_f32_kernel<<<(n + 255) / 256, 256, 0, s>>>(g, o, n);
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
 }  // namespace acehip

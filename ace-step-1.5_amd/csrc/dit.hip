@@ -73,7 +73,7 @@ struct acehip_dit {
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
     bf16_t *gemv_act = nullptr;
-    float *gatef = nullptr;            // D: the fp32 AdaLN gate row of a hipBLASLt projection (ACEHIP_BLASLT)        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
+    float *modf = nullptr;             // fp32 copy of mod: the AdaLN gate rows as hipBLASLt α vectors (ACEHIP_BLASLT)        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
     // constant V row and their cross-O output the per-layer constant cnull[l]
@@ -342,7 +342,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)L);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->gemv_act = A((size_t)16 * D);
-    h->gatef = (float *)A((size_t)2 * D);
+    h->modf = (float *)A((size_t)L * Bc * 6 * D * 2);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
     h->sk_part = (float *)A(SK_PART_BYTES / 2);
     h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
@@ -751,7 +751,8 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // timestep MLPs (temb, proj), unless acehip_dit_forward_step already broadcast the
     // schedule's precomputed row into h->temb / h->proj
     if (!ts_cached) RUN(timestep_mlps(h, h->emb, Bc, h->h1, h->temb_e, h->proj_e, h->temb, h->proj, s));
-    RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s));
+    const int ltm = blaslt_mask();
+    RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s, (ltm & 2) ? h->modf : nullptr));
     RUN(modulation(h->sst_out, 1, 2, h->temb, Bc, D, h->mod_out, s));
 
     // proj_in (base:1347-1358) over the packed patches Xin
@@ -774,17 +775,15 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // self-O / down (bit 2: gate as the α vector, needs one gate row for every batch row:
     // the schedule's broadcast timestep), cross-O (bit 4).  blaslt_gemm returning 1 (no plan)
     // falls through to the hand-written kernel.
-    const int ltm = blaslt_mask();
     const bool gate_uniform = ts_cached || Bc == 1;
-    auto lt_gated = [&](const bf16_t *Aop, int64_t lda, const bf16_t *Wop, int rows, int K, const bf16_t *gate) {
-        int rc2 = gate_to_f32(gate, h->gatef, D, s);
-        if (rc2) return rc2;
-        return blaslt_gemm(Aop, lda, Wop, K, h->X, D, rows, D, K, h->gatef, 1.0f, s);
+    auto lt_gated = [&](const bf16_t *Aop, int64_t lda, const bf16_t *Wop, int rows, int K, const float *gate) {
+        return blaslt_gemm(Aop, lda, Wop, K, h->X, D, rows, D, K, gate, 1.0f, s);
     };
     for (int l = 0; l < L; ++l) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
         const int64_t mbs = 6 * D;
+        const float *mdf = h->modf + (size_t)l * Bc * 6 * D;   // batch row 0's gates (gate_uniform)
         // --- self-attention with AdaLN-Zero (base:499-511); layer 0 of identical CFG rows: row 0
         const int Bs = (dup && l == 0) ? 1 : Bc, Ms = Bs * S;
         RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, Ms, D, eps, s, pend));
@@ -820,7 +819,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         const bool defer_o = fuse_rowadd && Bs == Bc && (Mq == M || Mq == 0);
         RUN(timed(h, 3, s, [&] {
             if ((ltm & 2) && Ms > 256 && gate_uniform) {
-                const int r2 = lt_gated(h->AO, qd, ly.wo, Ms, qd, md + 2 * D);
+                const int r2 = lt_gated(h->AO, qd, ly.wo, Ms, qd, mdf + 2 * D);
                 if (r2 <= 0) return r2;
             }
             return hgemm(h, o, s, defer_o ? &pend : nullptr);
@@ -877,7 +876,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
         RUN(timed(h, 1, s, [&] {
             if ((ltm & 2) && M > 256 && gate_uniform) {
-                const int r2 = lt_gated(h->Hb, F, ly.wdown, M, F, md + 5 * D);
+                const int r2 = lt_gated(h->Hb, F, ly.wdown, M, F, mdf + 5 * D);
                 if (r2 <= 0) return r2;
             }
             return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr);

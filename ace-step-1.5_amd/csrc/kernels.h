@@ -79,7 +79,7 @@ int timestep_sinusoid(const float *t, const float *t_r, int t_stride, int use_di
 int add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *out, int64_t n, hipStream_t s);
 // mod[l][b][j][d] = bf16(table[l][j][d] + proj[b][j][d]) for all layers
 int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj, int Bc, int D,
-               bf16_t *mod, hipStream_t s);
+               bf16_t *mod, hipStream_t s, float *modf = nullptr);
 // proj_in input pack: X[b][s][k*192+c] = (c<128 ? ctx : xt)[b % Bx][2s+k][..] or 0
 int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
                  hipStream_t s);
@@ -123,7 +123,6 @@ int head_post(const HeadPostArgs &a, hipStream_t s);
 int blaslt_mask();
 int blaslt_gemm(const bf16_t *A, int64_t lda, const bf16_t *W, int64_t ldw, bf16_t *C, int64_t ldc, int M, int N,
                 int K, const float *alpha_vec, float beta, hipStream_t s);
-int gate_to_f32(const bf16_t *g, float *o, int n, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---
 // ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials
