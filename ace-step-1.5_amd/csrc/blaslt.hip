@@ -74,10 +74,12 @@ bool make_plan(LtCtx &c, LtPlan &p, int M, int N, int K, int64_t lda, int64_t ld
 }  // namespace
 
 // ACEHIP_BLASLT bit mask: 1 = QKV projection (+ standalone head_post), 2 = gated-residual
-// projections (self-O, down), 4 = plain-residual projection (cross-O).  Default 0.
+// projections (self-O, down), 4 = plain-residual projection (cross-O).  Default 2: 240 s song
+// (tools/ab_env_song.py, one process, profiles/r03n5_blaslt_song_ab.txt) DiT 492.6 ms hand-
+// written, 494.4 with 1 (the standalone head_post eats the QKV gain), 481.8 with 2, 493.4 with 4.
 int blaslt_mask() {
     const char *e = getenv("ACEHIP_BLASLT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
 }
 
 // C = α ⊙ (A·Wᵀ) + β·C (α: per-column device vector alpha_vec[N], or 1 when null).  Returns 0
