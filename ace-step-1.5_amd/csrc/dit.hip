@@ -73,6 +73,7 @@ struct acehip_dit {
     bf16_t *Kc, *Vc, *E, *KVtmp;
     bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
     bf16_t *gemv_act = nullptr;
+    bool t_uniform = false;            // every batch row at one timestep (one AdaLN gate row): set per forward
     float *modf = nullptr;             // fp32 copy of mod: the AdaLN gate rows as hipBLASLt α vectors (ACEHIP_BLASLT)        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
@@ -682,10 +683,13 @@ static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, 
     // block run on row 0 only and are copied (ACEHIP_DIT_DEDUP=0 disables, for A/B)
     const char *de = getenv("ACEHIP_DIT_DEDUP");
     const bool dup = Bx == 1 && Bc > 1 && (ts_cached || t_stride == 0) && !(de && de[0] == '0');
+    // one timestep for every row (the schedule's broadcast row, or a broadcast t): forward and
+    // forward_step then take the same projection paths (hipBLASLt gated residual)
+    h->t_uniform = ts_cached || t_stride == 0;
     if (!h->graph_on || h->prof) {
         RUN(forward_body(h, Bc, S, dup, ts_cached, s));
     } else {
-        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), (dup ? 1 : 0) | (ts_cached ? 2 : 0),
+        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), (dup ? 1 : 0) | (ts_cached ? 2 : 0) | (h->t_uniform ? 4 : 0),
                             knob_hash()};
         if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
             if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
@@ -775,7 +779,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // self-O / down (bit 2: gate as the α vector, needs one gate row for every batch row:
     // the schedule's broadcast timestep), cross-O (bit 4).  blaslt_gemm returning 1 (no plan)
     // falls through to the hand-written kernel.
-    const bool gate_uniform = ts_cached || Bc == 1;
+    const bool gate_uniform = h->t_uniform || Bc == 1;
     auto lt_gated = [&](const bf16_t *Aop, int64_t lda, const bf16_t *Wop, int rows, int K, const float *gate) {
         return blaslt_gemm(Aop, lda, Wop, K, h->X, D, rows, D, K, gate, 1.0f, s);
     };

@@ -910,6 +910,11 @@ def test_blaslt_projections(gpu_device, monkeypatch):
     for m in ("7", "1", "2", "4"):
         assert rel_l2(outs[m].cpu(), outs["0"].cpu()) < 1e-2, m      # two bf16 chains (oracle bar: 0.025)
     assert not torch.equal(outs["2"], outs["0"])            # the hipBLASLt path actually ran
+    # forward(t[i]) (one broadcast t) takes the same paths as forward_step(i): bit-identical
+    monkeypatch.setenv("ACEHIP_BLASLT", "2")
+    a = rt.forward(xt, ctx, torch.tensor([0.3], device=gpu_device)).float()
+    torch.cuda.synchronize()
+    assert torch.equal(a, outs["2"])
     rt.close()
 
 
