@@ -16,11 +16,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libacehip.s
 ACEHIP_F32 = 0
 ACEHIP_BF16 = 1
 # include/acehip.h ACEHIP_VERSION this binding's signatures were written against
-ABI_VERSION = 300
+ABI_VERSION = 400
 
 # every symbol include/acehip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "acehip_get_version", "acehip_last_error",
+    "acehip_get_version", "acehip_last_error", "acehip_reload_knobs",
     "acehip_dit_create", "acehip_dit_set_weight", "acehip_dit_finalize",
     "acehip_dit_set_condition", "acehip_dit_set_uniform_rows", "acehip_dit_forward", "acehip_dit_destroy",
     "acehip_dit_set_graph", "acehip_dit_set_timesteps", "acehip_dit_forward_step",
@@ -66,6 +66,7 @@ def _declare(lib):
     sig = {
         "acehip_get_version": (c_int, []),
         "acehip_last_error": (c_char_p, []),
+        "acehip_reload_knobs": (c_int, []),
         "acehip_dit_create": (c_int, [c_int, POINTER(DiTCfg), POINTER(c_void_p)]),
         "acehip_dit_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
         "acehip_dit_finalize": (c_int, [P]),
@@ -140,6 +141,11 @@ def lib():
 def missing_exports():
     l = lib()
     return [n for n in EXPORTS if not hasattr(l, n)]
+
+
+def reload_knobs():
+    """Re-read the ACEHIP_* A/B switches after changing the environment (tests / A/B tools)."""
+    check(lib().acehip_reload_knobs(), "reload_knobs")
 
 
 def check(rc: int, what: str = ""):

@@ -144,8 +144,14 @@ class OobleckBackend:
         (tests/test_gpu_long.py windows); ``chunk_size`` / ``overlap`` are accepted and
         ignored.  The Gaussian draw is one ``randn`` over the whole latent, where the
         reference draws per chunk — the same distribution, as in its own
-        ``samples <= chunk_size`` branch."""
-        del chunk_size, overlap
+        ``samples <= chunk_size`` branch.  Placement follows the reference: a source of at most
+        ``chunk_size`` samples (default 30 s, 15 s on a GPU of ≤ 8 GB, vae_encode.py:46-53)
+        comes back on the device whatever ``offload_latent_to_cpu`` says (vae_encode.py:62-68);
+        longer ones are offloaded when it is set."""
+        del overlap
+        if chunk_size is None:
+            mem_gb = torch.cuda.get_device_properties(self.device).total_memory / 1024 ** 3
+            chunk_size = 48000 * 15 if mem_gb <= 8 else 48000 * 30
         was_2d = audio.dim() == 2
         if was_2d:
             audio = audio.unsqueeze(0)
@@ -155,7 +161,7 @@ class OobleckBackend:
         z = self.encode_tensor(audio, sample=True)
         if was_2d:
             z = z.squeeze(0)
-        return z.cpu() if offload_latent_to_cpu else z
+        return z.cpu() if offload_latent_to_cpu and audio.shape[-1] > chunk_size else z
 
     def encode(self, wav: torch.Tensor):
         """diffusers-style: ``.encode(x).latent_dist.sample()`` / ``.mode()``."""

@@ -78,7 +78,6 @@ struct SplitArgs {
     float *ws;     // ≥ (units − full)·nsplit·8·66·64 floats
     int *cnt;      // ≥ units − full ints, zero between launches
     int units = 0; // attn_pw_kernel: > 0 = persistent over units [0, units) (no splits)
-    int dbg = 0;   // timing experiments only (ACEHIP_ATTN_DBG, wrong results): 1 = tail parts skip the hand-off
 };
 
 // ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
@@ -551,7 +550,6 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     }
     if (DEFER && pending) pv_slot(pend_slot, pf);
 
-    if (nsplit > 1 && (sp.dbg & 1)) return;
     if (nsplit > 1) {
         // publish this part's (O, m, l) (slab_store: write-through 16-B stores), then take a
         // ticket; the last part merges every part in part order, its own from registers — no
@@ -794,17 +792,11 @@ __device__ __forceinline__ void pw_oscale(float a) {
 // fillers hide per MFMA gap) — attn_fwd_kernel's two waves per SIMD instead run the same
 // phase between barriers.  Same work units, tail split, LDS image, swapped Sᵀ = K·Qᵀ
 // layout and lazy rescale as attn_fwd_kernel.
-//
-// SHIFT (band only; no split, no persistence; ACEHIP_ATTN_SHIFT): each wave walks its OWN band
-// tiles instead of the workgroup's union — the odd waves (rows q0 + 64 ..) run one KV tile
-// ahead of the even ones in a 4-slot ring, so a unit takes max(own tiles) iterations instead of
-// the union's (one fewer) and both waves' masked edge tiles fall in the same iterations.
-template <int SHIFT>
 __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restrict__ q, const bf16_t *__restrict__ k,
                                                          const bf16_t *__restrict__ v, bf16_t *__restrict__ o,
                                                          int H, int KV, int Sq, int Sk, int window, float sl2,
                                                          int64_t o_ld, SplitArgs sp) {
-    constexpr int NBUF = SHIFT ? 4 : 2, TILE = KT * 256;
+    constexpr int NBUF = 2, TILE = KT * 256;
     __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * TILE];
     // wave index provably uniform (readfirstlane), so every per-wave tile decision below is a
     // scalar branch (a divergent-looking one makes hipcc structurize both tile variants into
@@ -880,25 +872,6 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         c_nt = g.ntiles;
         c_q0 = g.q0;
     }
-    // SHIFT: the stream is the union [s_a, s_a + s_n) of the two row blocks' tile ranges; this
-    // wave's own range starts at c_tf = s_a + d (d = 0 or 1: QB / 2 = KT) and runs c_nt tiles;
-    // s_it iterations (wave-uniform scalars)
-    int s_a = 0, s_n = 0, s_it = 0;
-    if constexpr (SHIFT) {
-        const int qblk = c_q0 - (wave & 1) * 64;
-        int a[2], n[2];
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-            const int lo = max(0, qblk + 64 * w - window), hi = min(Sk, qblk + 64 * w + 64 + window);
-            a[w] = lo / KT;
-            n[w] = max(0, (hi + KT - 1) / KT - a[w]);
-        }
-        s_a = a[0];
-        s_n = max(a[0] + n[0], a[1] + n[1]) - s_a;
-        s_it = max(n[0], n[1]);
-        c_tf = a[wave & 1];
-        c_nt = n[wave & 1];
-    }
     int qi[2] = {c_q0 + r, c_q0 + 32 + r};
 
     // O = 0 and Q → AGPRs (the clobber of a0 / a255 makes the kernel descriptor allocate all 256)
@@ -959,15 +932,10 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
                            kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
 
     float m[2] = {NEG, NEG}, l[2] = {0.f, 0.f};
-    // SHIFT: byte offsets of the ring slots of this wave's current tile (V) and next tile (K), and
-    // the stream tile staged after the current iteration's barrier (the slot is a run-time value)
-    uint32_t vsl = 0, ksl = 0;
-    int st_t = 0;
     // K read i (0..15) of ring slot SLOT into the K AGPRs
     auto k_read = [&](auto SLOTC, auto IC_) __attribute__((always_inline)) {
         constexpr int KB = decltype(SLOTC)::value * TILE, i = decltype(IC_)::value;
-        if constexpr (SHIFT) pw_kread<PW_K + 4 * i, (i >> 3) * 32 * 256>(koff[i & 7] + ksl);
-        else pw_kread<PW_K + 4 * i, KB + (i >> 3) * 32 * 256>(koff[i & 7]);
+        pw_kread<PW_K + 4 * i, KB + (i >> 3) * 32 * 256>(koff[i & 7]);
     };
     auto tile_barrier = [&] __attribute__((always_inline)) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1001,8 +969,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
 #if PW_X_NOVREAD
             rv[dt][t][s][h8] = opaque_s16x4();
 #else
-            if constexpr (SHIFT) rv[dt][t][s][h8] = ds_read_tr16_imm<(32 * t + 16 * s) * 256>(voff[dt][h8] + vsl);
-            else rv[dt][t][s][h8] = ds_read_tr16_imm<VB + (32 * t + 16 * s) * 256>(voff[dt][h8]);
+            rv[dt][t][s][h8] = ds_read_tr16_imm<VB + (32 * t + 16 * s) * 256>(voff[dt][h8]);
 #endif
         };
         auto v_wait = [&] __attribute__((always_inline)) {
@@ -1134,9 +1101,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
             load_q(geom(un, 0, 1));
         }
 #if !PW_X_NODMA
-        if constexpr (SHIFT) {
-            if (st_t < s_a + s_n) stage_tile(kv_src, st_t * KT, st_t & 3);
-        } else if (it + 2 < c_nt) stage_tile(kv_src, kv0 + 2 * KT, SLOT);
+        if (it + 2 < c_nt) stage_tile(kv_src, kv0 + 2 * KT, SLOT);
         else if (has_next && it + 2 - c_nt < n_nt) stage_tile(nx_src, (n_tf + it + 2 - c_nt) * KT, SLOT);
 #endif
         const bool more = it + 1 < c_nt || has_next;
@@ -1164,24 +1129,15 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
     // band: tiles outside the band of all 64 rows skipped; tiles inside it for all 64 mask-free
     auto run_tile = [&](int it, auto SLOTC) __attribute__((always_inline)) {
         const int kv0 = (c_tf + it) * KT, q0 = c_q0;
-        const bool outside = (SHIFT && it >= c_nt) || (window >= 0 && (kv0 > q0 + 63 + window || kv0 + KT - 1 < q0 - window));
+        const bool outside = window >= 0 && (kv0 > q0 + 63 + window || kv0 + KT - 1 < q0 - window);
         const bool interior = kv0 + KT <= Sk && (window < 0 || (kv0 >= q0 + 63 - window && kv0 + KT - 1 <= q0 + window));
         if (interior) tile(it, SLOTC, IC<0>{}, outside);
         else tile(it, SLOTC, IC<1>{}, outside);
     };
-    // prologue: tile 0 staged and visible, tile 1 in flight, K(0) read (SHIFT: stream tiles 0, 1
-    // visible, 2 in flight — the odd waves' first tile may be stream tile 1)
-    if constexpr (SHIFT) {
-        if (s_n > 0) stage_tile(kv_src, s_a * KT, s_a & 3);
-        if (s_n > 1) stage_tile(kv_src, (s_a + 1) * KT, (s_a + 1) & 3);
-        tile_barrier();
-        if (s_n > 2) stage_tile(kv_src, (s_a + 2) * KT, (s_a + 2) & 3);
-        ksl = (uint32_t)(c_tf & 3) * TILE;
-    } else {
-        if (c_nt > 0) stage_tile(kv_src, c_tf * KT, 0);
-        tile_barrier();
-        if (c_nt > 1) stage_tile(kv_src, (c_tf + 1) * KT, 1);
-    }
+    // prologue: tile 0 staged and visible, tile 1 in flight, K(0) read
+    if (c_nt > 0) stage_tile(kv_src, c_tf * KT, 0);
+    tile_barrier();
+    if (c_nt > 1) stage_tile(kv_src, (c_tf + 1) * KT, 1);
     if (c_nt > 0) sfor<0, 16>([&](auto G) __attribute__((always_inline)) { k_read(IC<0>{}, G); });
     int gpos = 0;   // position of the current tile in the workgroup's tile stream: ring slot gpos & 1
     for (;;) {
@@ -1193,21 +1149,9 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         n_nt = g.ntiles;
         nx_src = kv_base(g);
     }
-    if constexpr (SHIFT) {
-        // iteration j: own tile c_tf + j (ring slot (c_tf + j) & 3), K of the next one read after
-        // the barrier, stream tile s_a + j + 3 staged (its slot's last reader finished before
-        // barrier j − 1: tile s_a + j − 1)
-        for (int j = 0; j < s_it; ++j) {
-            vsl = (uint32_t)((c_tf + j) & 3) * TILE;
-            ksl = (uint32_t)((c_tf + j + 1) & 3) * TILE;
-            st_t = s_a + j + 3;
-            run_tile(j, IC<0>{});
-        }
-    } else {
-        for (int it = 0; it < c_nt; ++it, ++gpos) {
-            if (gpos & 1) run_tile(it, IC<1>{});
-            else run_tile(it, IC<0>{});
-        }
+    for (int it = 0; it < c_nt; ++it, ++gpos) {
+        if (gpos & 1) run_tile(it, IC<1>{});
+        else run_tile(it, IC<0>{});
     }
 
     // O out of the AGPRs (the last MFMAs wrote them just before: XDL → read pad)
@@ -1218,7 +1162,6 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
         oacc[i >> 6][(i >> 4) & 3][i & 15] = pw_oread<PW_O + i>();
     });
 
-    if (nsplit > 1 && (sp.dbg & 1)) return;
     if (nsplit > 1) {
         // tail-split hand-off as in attn_fwd_kernel's first version (4-B agent-scope relaxed
         // atomics; pw runs split only off the production path): the 16-B slab form's register
@@ -1320,10 +1263,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
 static int num_cus_attn() {
     // ACEHIP_ATTN_CUS overrides the CU count the tail split plans for (tests use it
     // to exercise 3- and 4-way splits on small shapes)
-    if (const char *e = getenv("ACEHIP_ATTN_CUS")) {
-        const int v = atoi(e);
-        if (v > 0) return v;
-    }
+    if (knobs().attn_cus > 0) return knobs().attn_cus;
     static int n = 0;
     if (!n) {
         int dev = 0;
@@ -1335,16 +1275,12 @@ static int num_cus_attn() {
 }
 
 // short-sequence KV split (a grid of a few units, e.g. the 10 s song's cross-attention: 8
-// units): KV tiles per part.  ACEHIP_ATTN_SHORT_TPP (A/B; read per call).  Turbo 10 s cross
+// units): KV tiles per part.  ACEHIP_ATTN_SHORT_TPP (A/B).  Turbo 10 s cross
 // (11 tiles, 8 units; tools/gpu_r03z.sh, one process): 1 tile per part 28.5 µs, 2: 22.7, 3: 20.3
 // (DiT song 27.7 / 27.1 / 26.8 ms) — fewer, longer parts pay fewer hand-offs; 4 and 6 tiles
 // (after the slab hand-off, tools/gpu_r03m2.sh): 19.6 / 21.9 vs 19.7 µs, song 25.7 / 26.1 vs 25.6
 // ms; default 3
-static int short_tpp() {
-    const char *e = getenv("ACEHIP_ATTN_SHORT_TPP");
-    const int v = e ? atoi(e) : 3;
-    return v > 0 ? v : 3;
-}
+static int short_tpp() { return knobs().attn_short_tpp; }
 
 size_t attention_ws_bytes() {
     const size_t cus = std::max<size_t>(1024, (size_t)num_cus_attn());
@@ -1375,16 +1311,14 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // the layer kinds that use it (1 full, 2 band, 4 cross = window < 0 with Sk != Sq).  r02 A/B
     // (tools/bench_attn.py, one process, three boxes): band 46.4-48.4 vs 47.6-48.8 µs (kept),
     // full 166-189 vs 161-179 and B = 1 cross 30.5-31.8 vs 29.6-30.6 (stay on attn_fwd_kernel)
-    int pw_mask = 2;
-    if (const char *e = getenv("ACEHIP_ATTN_PW")) pw_mask = atoi(e);
+    const Knobs &kn = knobs();
+    const int pw_mask = kn.attn_pw;
     const int kind_bit = window >= 0 ? 2 : (Sk == Sq ? 1 : 4);
     if (grp == 2 && !kmask && window != ATTN_CAUSAL && (pw_mask & kind_bit)) {
         const int units = nq * KV * B;
         SplitArgs sp{nq, units, 1, nullptr, nullptr};
-        if (const char *e = getenv("ACEHIP_ATTN_DBG")) sp.dbg = atoi(e);
         const int tail = units % cus;
-        int split_min = 24;        // shortest KV loop (tiles) whose tail units are split over KV ranges
-        if (const char *e = getenv("ACEHIP_ATTN_PW_SPLIT")) split_min = atoi(e);
+        const int split_min = kn.attn_pw_split;   // shortest KV loop (tiles) whose tail units are split
         if (ws && unit_tiles >= split_min && units > cus && tail > 0 && tail <= cus / 2) {
             sp.full = units - tail;
             sp.nsplit = min(4, cus / tail);
@@ -1399,21 +1333,12 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         int grid = sp.full + (units - sp.full) * sp.nsplit;
         // band layers with more units than CUs: one persistent workgroup per CU walking units
         // blockIdx.x + k·grid as one KV-tile stream (every unit then has ≥ 2 tiles: window ≥ KT,
-        // Sq = Sk > 2·KT).  ACEHIP_ATTN_PERSIST=0 restores one workgroup per unit (A/B; per call)
-        // ACEHIP_ATTN_SHIFT=1: band layers on the per-wave-range kernel (one workgroup per unit;
-        // A/B, per call)
-        const char *se = getenv("ACEHIP_ATTN_SHIFT");
-        if (se && se[0] == '1' && sp.nsplit == 1 && window >= KT) {
-            attn_pw_kernel<1><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
-            HIP_TRY(hipGetLastError());
-            return 0;
-        }
-        const char *pe = getenv("ACEHIP_ATTN_PERSIST");
-        if (!(pe && pe[0] == '0') && sp.nsplit == 1 && window >= KT && Sq == Sk && Sq > 2 * KT && units > cus) {
+        // Sq = Sk > 2·KT).  ACEHIP_ATTN_PERSIST=0 restores one workgroup per unit (A/B)
+        if (kn.attn_persist && sp.nsplit == 1 && window >= KT && Sq == Sk && Sq > 2 * KT && units > cus) {
             sp.units = units;
             grid = cus;
         }
-        attn_pw_kernel<0><<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
+        attn_pw_kernel<<<grid, 256, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp);
         HIP_TRY(hipGetLastError());
         return 0;
     }
@@ -1423,7 +1348,6 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     const int nrep = split_heads ? 1 : grp;
     const int units = nq * KV * (grp / nrep) * B;
     SplitArgs sp{nq, units, 1, nullptr, nullptr};
-    if (const char *e = getenv("ACEHIP_ATTN_DBG")) sp.dbg = atoi(e);
     // one workgroup per CU: a partial last round of whole units is replaced by
     // tail units split over ⌊CUs / tail⌋ KV ranges (1.5 rounds instead of 2 at
     // 384 units on 256 CUs)

@@ -1258,37 +1258,19 @@ __global__ void cast_bf16_f32_kernel(const bf16_t *s, float *d, int64_t n) {
 
 // ACEHIP_CONV7=0 keeps the k=7 convolutions on the im2col conv_gemm / resunit128
 // kernels (A/B knob for the halo-staged conv7_kernel)
-bool use_conv7() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("ACEHIP_CONV7");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
+bool use_conv7() { return knobs().conv7 != 0; }
 
 // Which of the remaining convs run on the persistent counted-ring convp_kernel:
 // default the k = 1 convs (C ≥ 256, residual epilogue), ACEHIP_CONVP=1 every eligible conv,
 // =0 none.  Per-kernel rocprof of a 240 s decode (r02): k = 1 convs 4.55 vs 5.01 ms on
 // conv_gemm_kernel, the ConvTranspose phases 8.30 vs 7.44 ms (so they stay there)
 bool use_convp(const ConvArgs &a, int phases) {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("ACEHIP_CONVP");
-        v = e ? (e[0] == '1' ? 1 : 0) : 2;
-    }
+    const int v = knobs().convp;
     return v == 1 || (v == 2 && a.taps == 1 && phases == 1);
 }
 
 // ACEHIP_RU7=0 keeps the C = 128 residual units on conv7_kernel<FUSED> (A/B knob)
-bool use_ru7() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("ACEHIP_RU7");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
+bool use_ru7() { return knobs().ru7 != 0; }
 
 int num_cus_conv() {
     static int n = 0;

@@ -71,10 +71,9 @@ struct acehip_dit {
     bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *Xin, *O2;
     bf16_t *emb[2], *h1, *temb_e[2], *proj_e[2], *temb, *proj, *mod, *mod_out;
     bf16_t *Kc, *Vc, *E, *KVtmp;
+    int kv_group = 1;                  // layers per cross-K/V GEMM at set_condition (KVtmp holds that many)
     bf16_t *wckv_all = nullptr;        // every layer's cross K/V projection, [L][2·kvd][D] (one GEMM)
-    bf16_t *gemv_act = nullptr;
-    bool t_uniform = false;            // every batch row at one timestep (one AdaLN gate row): set per forward
-    float *modf = nullptr;             // fp32 copy of mod: the AdaLN gate rows as hipBLASLt α vectors (ACEHIP_BLASLT)        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
+    bf16_t *gemv_act = nullptr;        // 16 × D: bf16(silu(x)) rows of the timestep MLPs (gemv_small)
     // CFG null rows (acehip_dit_set_uniform_rows): batch rows >= uniform_from have an
     // encoder sequence that is one vector repeated, so their cross-attention is the
     // constant V row and their cross-O output the per-layer constant cnull[l]
@@ -86,8 +85,6 @@ struct acehip_dit {
     bf16_t *ts_temb = nullptr, *ts_proj = nullptr, *ts_scratch = nullptr;
     bf16_t *tmp;   // weight staging (fp32 → bf16 casts, host repacks)
     void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs (short songs / turbo)
-    float *sk_part = nullptr;  // stream-K partial tiles (gemm_sk_kernel) + ready flags (zeroed)
-    int *sk_flag = nullptr;
     size_t tmp_elems = 0;
 
     // optional per-kernel event timing (acehip_dit_profile)
@@ -126,7 +123,6 @@ struct acehip_dit {
 static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, hipStream_t s);
 static int timestep_mlps(acehip_dit *h, const bf16_t *const emb[2], int rows, bf16_t *h1, bf16_t *const temb_e[2],
                          bf16_t *const proj_e[2], bf16_t *temb, bf16_t *proj, hipStream_t s);
-static int knob_hash();
 static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, const float *t, const float *t_r,
                         int t_stride, int step, int Bc, int T, void *vt_out, hipStream_t s);
 static int create_f32(acehip_dit *h);
@@ -140,8 +136,6 @@ static int forward_f32(acehip_dit *h, const float *xt, const float *ctx, int Bx,
 static inline int hgemm(acehip_dit *h, GemmArgs g, hipStream_t s, RowAdd *defer = nullptr) {
     g.ws = h->gemm_ws;
     g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
-    g.sk_part = h->sk_part;
-    g.sk_flag = h->sk_flag;
     return gemm(g, s, defer);
 }
 
@@ -249,8 +243,7 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->sliding.resize(h->L);
     for (int i = 0; i < h->L; ++i) h->sliding[i] = cfg->sliding ? cfg->sliding[i] : ((i + 1) % 2);
     h->cfg.sliding = nullptr;
-    const char *ge = getenv("ACEHIP_DIT_GRAPH");
-    h->graph_on = ge && ge[0] == '1';
+    h->graph_on = knobs().dit_graph == 1;
     if (cfg->fp32) {
         h->f32 = true;
         h->graph_on = false;
@@ -340,14 +333,17 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     h->h1 = A(Bc * D); h->temb = A(Bc * D); h->proj = A(Bc * 6 * D);
     h->mod = A((size_t)L * Bc * 6 * D); h->mod_out = A(Bc * 2 * D);
     h->Kc = A((size_t)L * Bc * kvd * Le); h->Vc = A((size_t)L * Bc * kvd * Le);
-    h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)L);
+    // cross K/V scratch: the layers' K/V projections run as GEMMs over groups of kv_group layers
+    // (N = kv_group·2·kvd), the group sized so the scratch stays ≤ 256 MiB at max_Bc·max_Lenc
+    // (all 24 layers in one GEMM for a CFG song, one layer per GEMM at the 16 × 2048 maximum)
+    {
+        const size_t per_layer = Bc * Le * 2 * kvd * 2;
+        h->kv_group = (int)std::max<size_t>(1, std::min<size_t>((size_t)L, ((size_t)256 << 20) / per_layer));
+    }
+    h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)h->kv_group);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
     h->gemv_act = A((size_t)16 * D);
-    h->modf = (float *)A((size_t)L * Bc * 6 * D * 2);
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
-    h->sk_part = (float *)A(SK_PART_BYTES / 2);
-    h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
-    if (h->sk_flag && hipMemset(h->sk_flag, 0, SK_MAX_BLOCKS * 4) != hipSuccess) ok = false;
     h->rope_cos = A(S * 128); h->rope_sin = A(S * 128);
     h->tmp_elems = std::max<size_t>((size_t)6 * D * D, (size_t)D * 384);
     h->tmp = A(h->tmp_elems * 2);   // room for an fp32 staging copy
@@ -518,17 +514,23 @@ int acehip_dit_set_condition(acehip_dit *h, const void *enc, int Bc, int Lenc, v
     int rc = hgemm(h, g, s);
     if (rc) return rc;
     const size_t per = (size_t)Bc * kvd * Lenc;
-    // every layer's K/V projection in one GEMM: M = Bc·Lenc rows × N = L·2·kvd (turbo 10 s:
-    // 641 × 49152 — a full-chip grid, where L separate N = 2048 GEMMs were small-M split-K
-    // launches + their epilogues); the k-norm / head-major scatter stays per layer
-    const int64_t ldkv = (int64_t)h->L * 2 * kvd;
-    GemmArgs k{};
-    k.A = h->E; k.lda = D; k.W = h->wckv_all; k.ldw = D; k.C = h->KVtmp; k.ldc = ldkv;
-    k.M = M; k.N = (int)ldkv; k.K = D; k.epi = EPI_STORE;
-    if ((rc = hgemm(h, k, s))) return rc;
+    // the layers' K/V projections in GEMMs over groups of kv_group layers: M = Bc·Lenc rows ×
+    // N = kv_group·2·kvd (turbo 10 s: 641 × 49152 in one GEMM — a full-chip grid, where L
+    // separate N = 2048 GEMMs were small-M split-K launches + their epilogues); the k-norm /
+    // head-major scatter stays per layer
+    const int G = h->kv_group;
+    const int64_t ldkv = (int64_t)G * 2 * kvd;
     for (int l = 0; l < h->L; ++l) {
+        const int lg = l % G;
+        if (lg == 0) {
+            const int nl = std::min(G, h->L - l);
+            GemmArgs k{};
+            k.A = h->E; k.lda = D; k.W = h->wckv_all + (size_t)l * 2 * kvd * D; k.ldw = D; k.C = h->KVtmp;
+            k.ldc = ldkv; k.M = M; k.N = nl * 2 * kvd; k.K = D; k.epi = EPI_STORE;
+            if ((rc = hgemm(h, k, s))) return rc;
+        }
         HeadPostArgs p{};
-        p.src = h->KVtmp + (size_t)l * 2 * kvd; p.ld_src = ldkv; p.B = Bc; p.S = Lenc;
+        p.src = h->KVtmp + (size_t)lg * 2 * kvd; p.ld_src = ldkv; p.B = Bc; p.S = Lenc;
         p.nq = 0; p.nk = h->cfg.kv_heads; p.nv = h->cfg.kv_heads;
         p.kw = h->layers[l].ckn; p.k = h->Kc + l * per; p.v = h->Vc + l * per;
         p.S_dst = Lenc; p.eps = h->cfg.eps;
@@ -643,22 +645,6 @@ int acehip_dit_forward_step(acehip_dit *h, const void *xt, const void *ctx, int 
 
 }  // extern "C"
 
-// hash of the A/B environment knobs the captured forward body reads (GEMM / split-K /
-// attention / row-add variants): a change re-captures the graph instead of replaying a
-// stale one
-static int knob_hash() {
-    // every ACEHIP_* variable of the environment (the kernels read their A/B knobs
-    // from getenv at launch time, e.g. ACEHIP_ATTN_PW_SPLIT in attention.hip), so a
-    // knob added anywhere in the library can never be missing from the graph key
-    uint32_t h = 2166136261u;                      // FNV-1a over the "NAME=value" entries
-    for (char **e = environ; e && *e; ++e) {
-        if (strncmp(*e, "ACEHIP_", 7) != 0) continue;
-        for (const char *c = *e; *c; ++c) h = (h ^ (uint8_t)*c) * 16777619u;
-        h = (h ^ (uint8_t)';') * 16777619u;
-    }
-    return (int)(h & 0x7fffffff);
-}
-
 // Everything of one forward between the input packing and proj_out: reads only handle
 // buffers (emb, Xin, weights, K/V cache), so it can be captured once and replayed.
 // bf16 forward; step >= 0 takes the timestep MLP outputs from the set_timesteps cache
@@ -681,21 +667,14 @@ static int forward_bf16(acehip_dit *h, const void *xt, const void *ctx, int Bx, 
     // CFG: every batch row reads xt/ctx row 0 (Bx = 1) at one broadcast t, so the rows are
     // identical until the first cross-attention — proj_in and layer 0's self-attention
     // block run on row 0 only and are copied (ACEHIP_DIT_DEDUP=0 disables, for A/B)
-    const char *de = getenv("ACEHIP_DIT_DEDUP");
-    const bool dup = Bx == 1 && Bc > 1 && (ts_cached || t_stride == 0) && !(de && de[0] == '0');
-    // one timestep for every row (the schedule's broadcast row, or a broadcast t): forward and
-    // forward_step then take the same projection paths (hipBLASLt gated residual)
-    h->t_uniform = ts_cached || t_stride == 0;
+    const bool dup = Bx == 1 && Bc > 1 && (ts_cached || t_stride == 0) && knobs().dit_dedup;
     if (!h->graph_on || h->prof) {
         RUN(forward_body(h, Bc, S, dup, ts_cached, s));
     } else {
-        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), (dup ? 1 : 0) | (ts_cached ? 2 : 0) | (h->t_uniform ? 4 : 0),
-                            knob_hash()};
+        const int key[6] = {Bc, S, h->cond_Lenc, std::min(h->uniform_from, Bc), (dup ? 1 : 0) | (ts_cached ? 2 : 0),
+                            (int)knobs().gen};   // a knob reload re-captures
         if (!h->gexec || memcmp(key, h->gkey, sizeof(key))) {
             if (h->gexec) { HIP_TRY(hipGraphExecDestroy(h->gexec)); h->gexec = nullptr; }
-            // ACEHIP_BLASLT: one eager pass first, so the hipBLASLt handle, workspace, plans and
-            // code objects exist before the capture (the graph then replays the same body)
-            if (blaslt_mask()) RUN(forward_body(h, Bc, S, dup, ts_cached, s));
             if (!h->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
             HIP_TRY(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
             const int brc = forward_body(h, Bc, S, dup, ts_cached, h->cap_stream);
@@ -755,8 +734,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // timestep MLPs (temb, proj), unless acehip_dit_forward_step already broadcast the
     // schedule's precomputed row into h->temb / h->proj
     if (!ts_cached) RUN(timestep_mlps(h, h->emb, Bc, h->h1, h->temb_e, h->proj_e, h->temb, h->proj, s));
-    const int ltm = blaslt_mask();
-    RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s, (ltm & 2) ? h->modf : nullptr));
+    RUN(modulation(h->tables, L, 6, h->proj, Bc, D, h->mod, s));
     RUN(modulation(h->sst_out, 1, 2, h->temb, Bc, D, h->mod_out, s));
 
     // proj_in (base:1347-1358) over the packed patches Xin
@@ -765,8 +743,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     g.M = dup ? S : M; g.N = D; g.K = 384; g.epi = EPI_STORE; g.bias = h->bin;
     RUN(hgemm(h, g, s));
 
-    const char *fe = getenv("ACEHIP_FUSE_ROWADD");
-    const bool fuse_rowadd = !(fe && fe[0] == '0');
+    const bool fuse_rowadd = knobs().fuse_rowadd != 0;
     const size_t cper = (size_t)Bc * kvd * Le;
     const int Bq = std::min(h->uniform_from, Bc), Mq = Bq * S;   // rows with a real cross-attention
     // small-M grids take gemm's split-K path; the residual epilogue of such a GEMM (O, cross-O,
@@ -774,20 +751,10 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
     // it (gemm sets pend.part only when it deferred).  Deferral needs that norm to cover every
     // row the GEMM wrote, and no X copy in between (the layer-0 CFG dedup).
     RowAdd pend{};
-    // ACEHIP_BLASLT (A/B, blaslt.hip): hipBLASLt for the large-M projections — QKV (bit 1: into
-    // Hb, free between the down projection and the next SwiGLU, + the standalone head_post),
-    // self-O / down (bit 2: gate as the α vector, needs one gate row for every batch row:
-    // the schedule's broadcast timestep), cross-O (bit 4).  blaslt_gemm returning 1 (no plan)
-    // falls through to the hand-written kernel.
-    const bool gate_uniform = h->t_uniform || Bc == 1;
-    auto lt_gated = [&](const bf16_t *Aop, int64_t lda, const bf16_t *Wop, int rows, int K, const float *gate) {
-        return blaslt_gemm(Aop, lda, Wop, K, h->X, D, rows, D, K, gate, 1.0f, s);
-    };
     for (int l = 0; l < L; ++l) {
         const auto &ly = h->layers[l];
         const bf16_t *md = h->mod + (size_t)l * Bc * 6 * D;
         const int64_t mbs = 6 * D;
-        const float *mdf = h->modf + (size_t)l * Bc * 6 * D;   // batch row 0's gates (gate_uniform)
         // --- self-attention with AdaLN-Zero (base:499-511); layer 0 of identical CFG rows: row 0
         const int Bs = (dup && l == 0) ? 1 : Bc, Ms = Bs * S;
         RUN(rmsnorm_mod(h->X, ly.n_sa, md + 0 * D, md + 1 * D, mbs, S, h->XN, Ms, D, eps, s, pend));
@@ -799,19 +766,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         q.hp.B = Bs; q.hp.S = S; q.hp.nq = H; q.hp.nk = KV; q.hp.nv = KV; q.hp.qw = ly.qn; q.hp.kw = ly.kn;
         q.hp.cos = h->rope_cos; q.hp.sin = h->rope_sin;
         q.hp.q = h->Qh; q.hp.k = h->Kh; q.hp.v = h->Vh; q.hp.S_dst = S; q.hp.eps = eps;
-        RUN(timed(h, 2, s, [&] {
-            if ((ltm & 1) && Ms > 256 && (size_t)F >= (size_t)q.N) {
-                const int r2 = blaslt_gemm(h->XN, D, ly.wqkv, D, h->Hb, q.N, Ms, q.N, D, nullptr, 0.0f, s);
-                if (r2 <= 0) {
-                    if (r2 < 0) return r2;
-                    HeadPostArgs hh = q.hp;
-                    hh.src = h->Hb;
-                    hh.ld_src = q.N;
-                    return head_post(hh, s);
-                }
-            }
-            return hgemm(h, q, s);
-        }));
+        RUN(timed(h, 2, s, [&] { return hgemm(h, q, s); }));
         RUN(timed(h, h->sliding[l] ? 5 : 4, s, [&] {
             return attention(h->Qh, h->Kh, h->Vh, h->AO, Bs, H, KV, S, S, h->sliding[l] ? h->cfg.window : -1,
                              scale, qd, h->attn_ws, s);
@@ -821,13 +776,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         o.M = Ms; o.N = D; o.K = qd; o.epi = EPI_GATED_RES; o.res = h->X; o.ldr = D;
         o.gate = md + 2 * D; o.gate_bstride = mbs; o.rows_per_batch = S;
         const bool defer_o = fuse_rowadd && Bs == Bc && (Mq == M || Mq == 0);
-        RUN(timed(h, 3, s, [&] {
-            if ((ltm & 2) && Ms > 256 && gate_uniform) {
-                const int r2 = lt_gated(h->AO, qd, ly.wo, Ms, qd, mdf + 2 * D);
-                if (r2 <= 0) return r2;
-            }
-            return hgemm(h, o, s, defer_o ? &pend : nullptr);
-        }));
+        RUN(timed(h, 3, s, [&] { return hgemm(h, o, s, defer_o ? &pend : nullptr); }));
         for (int b = Bs; b < Bc; ++b)
             HIP_TRY(hipMemcpyAsync(h->X + (size_t)b * S * D, h->X, (size_t)S * D * 2, hipMemcpyDeviceToDevice, s));
         // --- cross-attention, plain residual (base:513-526); rows >= uniform_from (CFG null
@@ -848,13 +797,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
             GemmArgs co{};
             co.A = h->AO; co.lda = qd; co.W = ly.wco; co.ldw = qd; co.C = h->X; co.ldc = D;
             co.M = Mq; co.N = D; co.K = qd; co.epi = EPI_RES; co.res = h->X; co.ldr = D;
-            RUN(timed(h, 3, s, [&] {
-                if ((ltm & 4) && Mq > 256) {
-                    const int r2 = blaslt_gemm(h->AO, qd, ly.wco, qd, h->X, D, Mq, D, qd, nullptr, 1.0f, s);
-                    if (r2 <= 0) return r2;
-                }
-                return hgemm(h, co, s, fuse_rowadd ? &pend : nullptr);
-            }));
+            RUN(timed(h, 3, s, [&] { return hgemm(h, co, s, fuse_rowadd ? &pend : nullptr); }));
         }
         // --- SwiGLU MLP with AdaLN-Zero (base:528-533); the null rows' constant cross-O output
         // is added inside the norm pass (ACEHIP_FUSE_ROWADD=0: separate add_row_bcast, A/B)
@@ -878,13 +821,7 @@ static int forward_body(acehip_dit *h, int Bc, int S, bool dup, bool ts_cached, 
         dn.A = h->Hb; dn.lda = F; dn.W = ly.wdown; dn.ldw = F; dn.C = h->X; dn.ldc = D;
         dn.M = M; dn.N = D; dn.K = F; dn.epi = EPI_GATED_RES; dn.res = h->X; dn.ldr = D;
         dn.gate = md + 5 * D; dn.gate_bstride = mbs; dn.rows_per_batch = S;
-        RUN(timed(h, 1, s, [&] {
-            if ((ltm & 2) && M > 256 && gate_uniform) {
-                const int r2 = lt_gated(h->Hb, F, ly.wdown, M, F, mdf + 5 * D);
-                if (r2 <= 0) return r2;
-            }
-            return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr);
-        }));
+        RUN(timed(h, 1, s, [&] { return hgemm(h, dn, s, fuse_rowadd ? &pend : nullptr); }));
     }
     // norm_out AdaLN (base:1491-1497); proj_out runs after the body
     RUN(rmsnorm_mod(h->X, h->norm_out, h->mod_out, h->mod_out + D, 2 * D, S, h->XN, M, D, eps, s, pend));
@@ -982,8 +919,7 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
     return gemm(g, (hipStream_t)stream);
 }
 
-// lazily allocated split-K and stream-K workspaces of the standalone kernel entry points
-// (one per device; the stream-K ready flags start zeroed and every launch leaves them zero)
+// lazily allocated split-K workspace of the standalone kernel entry points (one per device)
 static std::mutex g_abi_ws_mu;
 static void *abi_gemm_ws() {
     static std::map<int, void *> by_dev;
@@ -993,24 +929,6 @@ static void *abi_gemm_ws() {
     void *&ws = by_dev[dev];
     if (!ws && hipMalloc(&ws, GEMM_WS_BYTES) != hipSuccess) ws = nullptr;
     return ws;
-}
-static void abi_sk_ws(GemmArgs &g) {
-    static std::map<int, std::pair<float *, int *>> by_dev;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
-    std::lock_guard<std::mutex> lk(g_abi_ws_mu);
-    auto &e = by_dev[dev];
-    if (!e.first) {
-        void *p = nullptr, *f = nullptr;
-        if (hipMalloc(&p, SK_PART_BYTES) != hipSuccess) return;
-        if (hipMalloc(&f, SK_MAX_BLOCKS * 4) != hipSuccess || hipMemset(f, 0, SK_MAX_BLOCKS * 4) != hipSuccess) {
-            (void)hipFree(p);
-            return;
-        }
-        e = {(float *)p, (int *)f};
-    }
-    g.sk_part = e.first;
-    g.sk_flag = e.second;
 }
 
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc, int M, int N,
@@ -1024,17 +942,9 @@ int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C,
     else if (epi == 0) g.epi = EPI_STORE;
     else return fail(ACEHIP_E_ARG, "gemm_ex: epilogue");
     if (M <= 0 || N % 128 || K % 64) return fail(ACEHIP_E_ARG, "gemm_ex: shape");
-    if (variant >= 100) {   // small-M A/B: 100 + mode (gemm_small)
+    if (variant < 0) {   // production dispatch (split-K for small grids)
         g.ws = abi_gemm_ws();
         g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
-        return gemm_small(g, variant - 100, (hipStream_t)stream);
-    }
-    if (variant < 0 || variant == 14) {   // production dispatch (split-K, stream-K) / forced stream-K
-        g.ws = abi_gemm_ws();
-        g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
-        abi_sk_ws(g);
-        if (epi == 2) g.ldr = ldc;
-        if (variant == 14) return gemm_sk_forced(g, (hipStream_t)stream);
         return gemm(g, (hipStream_t)stream);
     }
     return gemm_variant(g, variant, (hipStream_t)stream);
@@ -1066,7 +976,6 @@ int acehip_gemm_headpost_bf16(const void *A, int lda, const void *W, int K, int 
     g.hp.q = (bf16_t *)q; g.hp.k = (bf16_t *)k; g.hp.v = (bf16_t *)v; g.hp.S_dst = S; g.hp.eps = eps;
     g.ws = abi_gemm_ws();
     g.ws_bytes = g.ws ? GEMM_WS_BYTES : 0;
-    abi_sk_ws(g);
     return gemm(g, (hipStream_t)stream);
 }
 

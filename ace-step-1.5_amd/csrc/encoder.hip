@@ -53,16 +53,12 @@ struct acehip_enc {
     bf16_t *X, *XN, *Qh, *Kh, *Vh, *AO, *Hb, *O128;
     void *attn_ws = nullptr;
     void *gemm_ws = nullptr;   // split-K partials for small-M GEMMs
-    float *sk_part = nullptr;  // stream-K partial tiles (gemm_sk_kernel) + ready flags (zeroed)
-    int *sk_flag = nullptr;
 };
 
 // every GEMM of this runtime may use the handle's split-K workspace (small-M grids)
 static inline int hgemm(acehip_enc *h, GemmArgs g, hipStream_t s, RowAdd *defer = nullptr) {
     g.ws = h->gemm_ws;
     g.ws_bytes = h->gemm_ws ? GEMM_WS_BYTES : 0;
-    g.sk_part = h->sk_part;
-    g.sk_flag = h->sk_flag;
     return gemm(g, s, defer);
 }
 
@@ -177,9 +173,6 @@ int acehip_enc_create(int device, const acehip_enc_cfg *cfg, acehip_enc **out) {
     h->Hb = A(M * F);
     h->O128 = cfg->out_dim ? A(M * 128) : nullptr;
     h->gemm_ws = A(GEMM_WS_BYTES / 2);
-    h->sk_part = (float *)A(SK_PART_BYTES / 2);
-    h->sk_flag = (int *)A(SK_MAX_BLOCKS * 2);
-    if (h->sk_flag && hipMemset(h->sk_flag, 0, SK_MAX_BLOCKS * 4) != hipSuccess) ok = false;
     h->rope_cos = A((size_t)cfg->max_S * 128); h->rope_sin = A((size_t)cfg->max_S * 128);
     if (ok) {
         const size_t wb = attention_ws_bytes();

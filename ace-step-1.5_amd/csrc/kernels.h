@@ -4,6 +4,31 @@
 
 namespace acehip {
 
+// ----------------------------------------------------------------- knobs ---
+// A/B switches (knobs.hip): read from the ACEHIP_* environment once, on first use or by
+// acehip_reload_knobs(); gen counts reloads (part of the DiT graph key)
+struct Knobs {
+    int gemm_tailsplit = 1;   // ACEHIP_GEMM_TAILSPLIT: 0 off, 1 on, 2..9 the tail tile variant
+    int gemm_w4s = 1;         // ACEHIP_GEMM_W4S: half-chip grids on the four-wave 192×128 tile
+    int gemm_hp128 = 1;       // ACEHIP_GEMM_HP128: 0 / 2 alternative cross-Q head-post paths
+    int splitk_fuse = 1;      // ACEHIP_SPLITK_FUSE: split-K epilogues folded into their consumers
+    int splitk_bn = 0;        // ACEHIP_SPLITK_BN: 0 auto, 64 / 128 forced
+    int smallm_wholek = 1;    // ACEHIP_SMALLM_WHOLEK: M ≤ 128 SwiGLU on whole-K 128×64 tiles
+    int attn_pw = 2;          // ACEHIP_ATTN_PW: layer kinds on attn_pw_kernel (1 full, 2 band, 4 cross)
+    int attn_persist = 1;     // ACEHIP_ATTN_PERSIST: persistent band units
+    int attn_pw_split = 24;   // ACEHIP_ATTN_PW_SPLIT: shortest KV loop whose tail units are split
+    int attn_short_tpp = 3;   // ACEHIP_ATTN_SHORT_TPP: KV tiles per part of the short split
+    int attn_cus = 0;         // ACEHIP_ATTN_CUS: CU count the splits plan for (0: the device's)
+    int fuse_rowadd = 1;      // ACEHIP_FUSE_ROWADD: null-row constant added in the MLP norm
+    int dit_dedup = 1;        // ACEHIP_DIT_DEDUP: layer-0 CFG row dedup
+    int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body
+    int conv7 = 1;            // ACEHIP_CONV7: halo-staged k = 7 VAE convs
+    int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
+    int ru7 = 1;              // ACEHIP_RU7: persistent C = 128 residual unit
+    unsigned gen = 0;
+};
+const Knobs &knobs();
+
 // ------------------------------------------------------------------ GEMM ---
 // per-head post-projection: q/k RMSNorm (+RoPE) and scatter to head-major layouts
 struct HeadPostArgs {
@@ -42,23 +67,16 @@ struct GemmArgs {
     // split-K workspace (grids too small to fill the chip): fp32 partials [splits][M][N]
     // + a bf16 [M][N] staging tile for the head-post case; null disables split-K
     void *ws; size_t ws_bytes;
-    // stream-K workspace (gemm_sk_kernel): SK_MAX_BLOCKS partial tiles of 256 KiB + as many
-    // ready flags (zeroed at allocation; every launch leaves them zero); null disables
-    float *sk_part; int *sk_flag;
     int kper;                       // internal: K-tiles per split (EPI_PARTIAL launches)
 };
-constexpr int EPI_PARTIAL = 5;
-constexpr int SK_MAX_BLOCKS = 256;
-constexpr size_t SK_PART_BYTES = (size_t)SK_MAX_BLOCKS << 18;   // 256 KiB per block
-constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace      // internal: store the fp32 accumulators of split blockIdx.y to ws
+constexpr int EPI_PARTIAL = 5;                       // internal: fp32 partials of split blockIdx.y → ws
+constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace
 struct RowAdd;
 // defer != null: a residual-epilogue GEMM (EPI_GATED_RES / EPI_RES) that takes the small-M
 // split-K path leaves its fp32 partials in a.ws and describes its epilogue in *defer (the
 // consumer rmsnorm_mod applies it, one launch fewer); defer->part stays null otherwise
 int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer = nullptr);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
-int gemm_small(const GemmArgs &a, int mode, hipStream_t s);        // small-M A/B (needs ws)
-int gemm_sk_forced(const GemmArgs &a, hipStream_t s);              // stream-K 256² tile (needs sk_*)
 // Launch-attached timing events for the next GEMM of this thread (the SwiGLU paths: ping-pong,
 // generic and four-wave tiles): its first launch takes `start`, every launch `stop` (the last
 // completion wins), by hipExtLaunchKernel — no separate event packets in the stream.
@@ -79,7 +97,7 @@ int timestep_sinusoid(const float *t, const float *t_r, int t_stride, int use_di
 int add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *out, int64_t n, hipStream_t s);
 // mod[l][b][j][d] = bf16(table[l][j][d] + proj[b][j][d]) for all layers
 int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj, int Bc, int D,
-               bf16_t *mod, hipStream_t s, float *modf = nullptr);
+               bf16_t *mod, hipStream_t s);
 // proj_in input pack: X[b][s][k*192+c] = (c<128 ? ctx : xt)[b % Bx][2s+k][..] or 0
 int pack_patches(const bf16_t *xt, const bf16_t *ctx, int Bx, int Bc, int T, int S, bf16_t *X,
                  hipStream_t s);
@@ -119,10 +137,6 @@ int rmsnorm_mod(const bf16_t *x, const bf16_t *w, const bf16_t *shift, const bf1
                 int64_t mod_bstride, int rows_per_batch, bf16_t *out, int M, int D, float eps,
                 hipStream_t s, RowAdd ra = RowAdd{}, int rows_per_wave = 0);
 int head_post(const HeadPostArgs &a, hipStream_t s);
-// hipBLASLt alternative for the N <= 4096 projections (blaslt.hip; ACEHIP_BLASLT bit mask)
-int blaslt_mask();
-int blaslt_gemm(const bf16_t *A, int64_t lda, const bf16_t *W, int64_t ldw, bf16_t *C, int64_t ldc, int M, int N,
-                int K, const float *alpha_vec, float beta, hipStream_t s);
 
 // ------------------------------------------------------------- attention ---
 // ws: attention_ws_bytes() of zero-initialised device memory (tail-split partials

@@ -94,7 +94,7 @@ __global__ void add_kernel(const bf16_t *a, const bf16_t *b, bf16_t *o, int64_t 
 
 // mod[l][b][j][d] = bf16(table[l][j][d] + proj[b][j % proj_rows][d])
 __global__ void modulation_kernel(const bf16_t *tables, int rows, const bf16_t *proj, int proj_rows,
-                                  int Bc, int D, bf16_t *mod, float *modf) {
+                                  int Bc, int D, bf16_t *mod) {
     const int l = blockIdx.z, b = blockIdx.y;
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)rows * D) return;
@@ -103,7 +103,6 @@ __global__ void modulation_kernel(const bf16_t *tables, int rows, const bf16_t *
                     bf2f(proj[((int64_t)b * proj_rows + (j % proj_rows)) * D + d]);
     const bf16_t r = f2bf(v);
     mod[(((int64_t)l * Bc + b) * rows) * D + e] = r;
-    if (modf) modf[(((int64_t)l * Bc + b) * rows) * D + e] = bf2f(r);   // fp32 copy of the bf16 value
 }
 
 // X[b][s][k*192 + c]: c < 128 → ctx[b%Bx][2s+k][c]; else xt[b%Bx][2s+k][c-128]; 0 past T
@@ -333,11 +332,11 @@ int add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *out, int64_t n, hipStream
 }
 
 int modulation(const bf16_t *tables, int n_tables, int rows, const bf16_t *proj, int Bc, int D,
-               bf16_t *mod, hipStream_t s, float *modf) {
+               bf16_t *mod, hipStream_t s) {
     // proj rows: 6 for the layer tables (proj [Bc][6][D]); 1 for norm_out (temb [Bc][D])
     const int proj_rows = rows == 6 ? 6 : 1;
     dim3 grid((unsigned)(((int64_t)rows * D + 255) / 256), Bc, n_tables);
-    modulation_kernel<<<grid, 256, 0, s>>>(tables, rows, proj, proj_rows, Bc, D, mod, modf);
+    modulation_kernel<<<grid, 256, 0, s>>>(tables, rows, proj, proj_rows, Bc, D, mod);
     HIP_TRY(hipGetLastError());
     return 0;
 }

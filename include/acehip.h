@@ -35,7 +35,7 @@ extern "C" {
  * entry points, acehip_dit_cfg.fp32 (round 2).  300: acehip_vae_encode accepts any
  * N in [hop, max_T*hop] (latents = floor(N/hop) frames).  Callers check
  * acehip_get_version() == ACEHIP_VERSION before binding (acehip/_ffi.py does). */
-#define ACEHIP_VERSION 300
+#define ACEHIP_VERSION 400
 
 enum acehip_status {
     ACEHIP_OK = 0,
@@ -49,6 +49,10 @@ enum acehip_status {
 enum acehip_dtype { ACEHIP_F32 = 0, ACEHIP_BF16 = 1 };
 
 int acehip_get_version(void);
+/* Re-read the ACEHIP_* A/B switches from the environment (they are read once, on first
+ * use, otherwise).  Tests and A/B tools only: call while no other thread is inside the
+ * library; a DiT handle re-captures its HIP graph after a reload. */
+int acehip_reload_knobs(void);
 const char *acehip_last_error(void);
 
 /* ---------------------------------------------------------------- DiT ---- */
@@ -340,14 +344,10 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
 
 /* Same with an explicit epilogue (0 store+bias, 2 residual add into C,
  * 3 SwiGLU: W rows packed [32 gate; 32 up] per 64-row panel, C is [M][N/2])
- * and tile variant (0: 128x128 2-stage, 1: 256x128 3-stage ring, 2: 128x128
- * 3-stage, 3: 128x256 3-stage, 4: 256x128 2-stage, 5: 256x256 2-stage,
- * 6: 192x256 2-stage, 7: 256x256 ping-pong, 8: 192x256 ping-pong; 3 and 5-8
- * need N % 256 == 0; -1: the production choice, including the weight-streaming
- * kernel for M <= 256 and split-K for grids that cannot fill half the chip;
- * 100 + d: the weight-streaming kernel with a d-deep register ring (d = 2..4),
- * 100: the 128x128 split-K path — small-M A/B; 14: the stream-K 256x256 ping-pong
- * tile, N % 256 == 0) — tuning and tests. */
+ * and tile variant (0: 128x128 2-stage, 7: 256x256 ping-pong, 8: 192x256
+ * ping-pong (N % 256 == 0), 13: four-wave 192x128 (N % 128 == 0), 16: 128x64
+ * 4-stage; -1: the production choice, including split-K for grids that cannot
+ * fill half the chip) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,
                         int M, int N, int K, const void *bias, int epi, int variant, void *stream);
 

@@ -46,3 +46,20 @@ def gpu_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def set_knob(monkeypatch, name, value):
+    """Set one ACEHIP_* A/B switch for this test: the library reads its knobs once, so the
+    environment change is followed by acehip_reload_knobs (undone by the next test's reload)."""
+    from acehip import _ffi
+    monkeypatch.setenv(name, str(value))
+    _ffi.reload_knobs()
+
+
+@pytest.fixture(autouse=True)
+def _fresh_knobs():
+    """Every test starts from the knobs of the (restored) environment."""
+    from acehip import _ffi
+    if _ffi._LIB is not None:
+        _ffi.reload_knobs()
+    yield

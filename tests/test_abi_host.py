@@ -21,7 +21,7 @@ def test_header_symbols_exported():
     missing = [s for s in sorted(declared) if not hasattr(lib, s)]
     assert not missing, missing
     assert set(_ffi.EXPORTS) == declared
-    assert lib.acehip_get_version() == 300 == _ffi.ABI_VERSION
+    assert lib.acehip_get_version() == 400 == _ffi.ABI_VERSION
 
 
 def test_error_paths_without_gpu():
@@ -134,8 +134,7 @@ def test_pw_kernel_agprs_stay_asm_owned(tmp_path):
     out = tmp_path / "attention.s"
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", src, "-o",
                     str(out)], check=True, capture_output=True)
-    # every instantiation (the band / full kernel and the SHIFT variant), each up to its
-    # .Lfunc_end label (early returns put several s_endpgm in one body)
+    # the kernel body up to its .Lfunc_end label (early returns put several s_endpgm in one body)
     bodies, body, in_asm, compiler_agpr = {}, None, False, []
     for line in out.read_text().splitlines():
         mk = re.match(r"^(_ZN6acehip12_GLOBAL__N_114attn_pw_kernel\S*):", line)
@@ -154,7 +153,7 @@ def test_pw_kernel_agprs_stay_asm_owned(tmp_path):
             in_asm = False
         elif not in_asm and re.search(r"v_accvgpr_(read|write)", line):
             compiler_agpr.append(line.strip())
-    assert len(bodies) >= 2, f"attn_pw_kernel instantiations not found in the assembly: {list(bodies)}"
+    assert len(bodies) >= 1, f"attn_pw_kernel not found in the assembly: {list(bodies)}"
     assert not compiler_agpr, f"hipcc uses AGPRs in attn_pw_kernel: {compiler_agpr[:4]}"
     for name, b in bodies.items():
         assert not any("scratch_" in ln for ln in b), f"{name} spills to scratch"

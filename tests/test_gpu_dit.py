@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import cosine, golden_manifest, load_golden, rel_l2
+from conftest import set_knob, cosine, golden_manifest, load_golden, rel_l2
 
 from acehip.config import DiTConfig
 from acehip.weights import synth_dit_weights
@@ -45,13 +45,13 @@ def test_gemm(gpu_device, M, N, K):
 EPI_STORE, EPI_GATED_RES, EPI_RES, EPI_SWIGLU = 0, 1, 2, 3
 
 
-@pytest.mark.parametrize("variant", list(range(14)))
+@pytest.mark.parametrize("variant", [0, 7, 8, 13, 16])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 64), (517, 256, 128), (200, 512, 192), (777, 768, 640)])
 def test_gemm_variants(gpu_device, variant, M, N, K):
-    """Every tile/schedule variant, odd K-tile counts (ring prologue/tail) and ragged M,
+    """Every production tile variant, odd K-tile counts (ring prologue/tail) and ragged M,
     plain store + SwiGLU epilogue (gate/up interleaved in 32-row panels)."""
     ff = _lib()
-    if variant in (3, 5, 6, 7, 8, 9, 10, 11, 12) and N % 256 or variant == 13 and N % 128:
+    if variant in (7, 8) and N % 256:
         pytest.skip("variant needs N % 256 == 0")
     g = torch.Generator(device="cpu").manual_seed(M * 3 + N + K + variant)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -80,8 +80,8 @@ def test_attention_tail_split(gpu_device, monkeypatch, cus, window, pw):
     """Tail balancing with 2-, 3- and 4-way KV splits (24 units; CU count 16/18/20 → tail 8/6/4 →
     nsplit 2/3/4; overridden so small
     shapes take the split path): merged partials must match the fp32 reference."""
-    monkeypatch.setenv("ACEHIP_ATTN_CUS", str(cus))
-    monkeypatch.setenv("ACEHIP_ATTN_PW", pw)
+    set_knob(monkeypatch, "ACEHIP_ATTN_CUS", str(cus))
+    set_knob(monkeypatch, "ACEHIP_ATTN_PW", pw)
     ff = _lib()
     B, H, KV, Sq, Sk = 2, 4, 2, 700, 1600       # 6 q-blocks x 2 KV x 2 = 24 units, 25 KV tiles
     g = torch.Generator(device="cpu").manual_seed(cus * 3 + window)
@@ -112,8 +112,8 @@ def test_attention_band_persistent(gpu_device, monkeypatch, cus, B, H, KV, S, wi
     ring parity between units; ragged S leaves a partial last tile); cus = 0 keeps the real
     CU count (the 240 s / 2- and 3-round shapes).  Bit-identical to one workgroup per unit."""
     if cus:
-        monkeypatch.setenv("ACEHIP_ATTN_CUS", str(cus))
-    monkeypatch.setenv("ACEHIP_ATTN_PW", "2")
+        set_knob(monkeypatch, "ACEHIP_ATTN_CUS", str(cus))
+    set_knob(monkeypatch, "ACEHIP_ATTN_PW", "2")
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(S + cus)
     q = torch.randn(B, H, S, 128, generator=g).to(gpu_device, torch.bfloat16)
@@ -121,41 +121,12 @@ def test_attention_band_persistent(gpu_device, monkeypatch, cus, B, H, KV, S, wi
     v = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
     outs = {}
     for pers in ("1", "0"):
-        monkeypatch.setenv("ACEHIP_ATTN_PERSIST", pers)
+        set_knob(monkeypatch, "ACEHIP_ATTN_PERSIST", pers)
         o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
         ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, S, S,
                                                 window, 1 / math.sqrt(128), ff.stream_ptr()))
         torch.cuda.synchronize()
         outs[pers] = o
-    ref = _attn_ref(q, k, v, window).transpose(1, 2).reshape(B, S, H * 128)
-    assert rel_l2(outs["1"].float().cpu(), ref.cpu()) < 1e-2
-    assert torch.equal(outs["1"], outs["0"])
-
-
-@pytest.mark.parametrize("B,H,KV,S,window", [(2, 4, 2, 1000, 128), (1, 16, 8, 777, 64), (1, 2, 1, 450, 200),
-                                          (2, 4, 2, 333, 65), (1, 4, 2, 130, 127), (2, 16, 8, 3000, 128),
-                                          (1, 2, 1, 200, 64)])
-def test_attention_band_shift(gpu_device, monkeypatch, B, H, KV, S, window):
-    """ACEHIP_ATTN_SHIFT=1: each wave of attn_pw_kernel walks its own band tiles (odd waves one
-    tile ahead in a 4-slot ring) instead of the workgroup's union.  Same tiles per row in the same
-    order as the union walk (whose extra tiles a wave skips), so bit-identical to it; windows
-    that are / are not multiples of KT, ragged S with a partial last tile, a band touching both
-    sequence ends."""
-    monkeypatch.setenv("ACEHIP_ATTN_PW", "2")
-    monkeypatch.setenv("ACEHIP_ATTN_PERSIST", "0")
-    ff = _lib()
-    g = torch.Generator(device="cpu").manual_seed(S + window)
-    q = torch.randn(B, H, S, 128, generator=g).to(gpu_device, torch.bfloat16)
-    k = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
-    v = torch.randn(B, KV, S, 128, generator=g).to(gpu_device, torch.bfloat16)
-    outs = {}
-    for shift in ("1", "0"):
-        monkeypatch.setenv("ACEHIP_ATTN_SHIFT", shift)
-        o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
-        ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, S, S,
-                                                window, 1 / math.sqrt(128), ff.stream_ptr()))
-        torch.cuda.synchronize()
-        outs[shift] = o
     ref = _attn_ref(q, k, v, window).transpose(1, 2).reshape(B, S, H * 128)
     assert rel_l2(outs["1"].float().cpu(), ref.cpu()) < 1e-2
     assert torch.equal(outs["1"], outs["0"])
@@ -192,7 +163,7 @@ def _attn_ref(q, k, v, window):
 def test_attention(gpu_device, monkeypatch, B, H, KV, Sq, Sk, window, pw):
     """pw: ACEHIP_ATTN_PW — "0" every layer kind on attn_fwd_kernel, "7" the GQA-pair unmasked
     kinds (full / band / cross) on the 64-row-per-wave attn_pw_kernel (production: band only)."""
-    monkeypatch.setenv("ACEHIP_ATTN_PW", pw)
+    set_knob(monkeypatch, "ACEHIP_ATTN_PW", pw)
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(Sq * 7 + Sk)
     q = torch.randn(B, H, Sq, 128, generator=g).to(gpu_device, torch.bfloat16)
@@ -230,6 +201,18 @@ def test_dit_forward_vs_reference_golden(gpu_device, name):
     ref = g["vt"].float()
     assert rel_l2(out, ref) <= TOL_REL, rel_l2(out, ref)
     assert cosine(out, ref) >= TOL_COS
+    if torch.equal(g["t"], g["t"][:1].expand(2)) and torch.equal(g["t_r"], g["t_r"][:1].expand(2)):
+        # one timestep for both rows (the sampler's t_curr·ones(Bc), base:1929-1941): a broadcast
+        # t (t_stride 0) and the schedule path (set_timesteps + forward_step) vs the same golden
+        xd, cd = g["xt"].to(gpu_device).contiguous(), g["ctx"].to(gpu_device).contiguous()
+        bc = rt.forward(xd, cd, g["t"][:1].float().to(gpu_device), g["t_r"][:1].float().to(gpu_device)).float().cpu()
+        rt.set_timesteps(torch.tensor([1.0, float(g["t"][0])], device=gpu_device),
+                         torch.tensor([1.0, float(g["t_r"][0])], device=gpu_device))
+        st = rt.forward_step(xd, cd, 1).float().cpu()
+        torch.cuda.synchronize()
+        for o in (bc, st):
+            assert rel_l2(o, ref) <= TOL_REL and cosine(o, ref) >= TOL_COS, rel_l2(o, ref)
+        assert torch.equal(bc, st)
     rt.close()
 
 
@@ -572,9 +555,8 @@ def test_weight_reload_matches_fresh_handle(gpu_device):
                                    (256, 12288, 2048), (200, 2048, 1088), (300, 2048, 2048)])
 def test_gemm_splitk_small_m(gpu_device, M, N, K):
     """Small-M paths (short songs / turbo): the production dispatch (variant -1: the
-    128×128 split-K path) with store, residual and SwiGLU epilogues, and the weight-
-    streaming skinny kernel (A/B variants 102-104: ring depth 2-4; M ≤ 256 in one or two
-    128-row chunks, rows past M read as zeros, 1–8 K splits)."""
+    128×128 / 128×64 split-K path, or whole-K 128×64 tiles for the M ≤ 128 SwiGLU) with
+    store, residual and SwiGLU epilogues."""
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -592,13 +574,6 @@ def test_gemm_splitk_small_m(gpu_device, M, N, K):
                                           ff.stream_ptr()))
     torch.cuda.synchronize()
     assert rel_l2(C2.float().cpu(), (R.float() + ref.bfloat16().float()).cpu()) < 5e-3
-    if M <= 256 and K % 128 == 0:
-        for v in (102, 103, 104):
-            Ck = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
-            ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Ck), N, M, N, K, None,
-                                                  EPI_STORE, v, ff.stream_ptr()))
-            torch.cuda.synchronize()
-            assert rel_l2(Ck.float().cpu(), ref.cpu()) < 5e-3, v
     Cs = torch.empty(M, N // 2, device=gpu_device, dtype=torch.bfloat16)
     ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cs), N // 2, M, N, K, None,
                                           EPI_SWIGLU, -1, ff.stream_ptr()))
@@ -606,54 +581,6 @@ def test_gemm_splitk_small_m(gpu_device, M, N, K):
     y = ref.bfloat16().float().view(M, N // 64, 2, 32)
     gate, up = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
     assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2
-
-
-@pytest.mark.parametrize("M,N,K", [(6000, 2048, 6144), (6000, 2048, 2048), (6000, 4096, 2048), (6000, 12288, 2048),
-                                   (15000, 2048, 6144), (1000, 512, 1024), (700, 768, 512)])
-def test_gemm_streamk(gpu_device, M, N, K):
-    """Stream-K 256×256 ping-pong tile (variant 14): every CU multiplies the same number of
-    K-tiles, tiles split between two CUs are finished by adding the contributor's fp32
-    partial (flag hand-off).  Store, residual and SwiGLU epilogues vs fp32 torch; twice in a
-    row (the ready flags must be left at zero for the next launch); the production dispatch
-    (-1) agrees.  Shapes whose split would need two contributors per tile are refused."""
-    ff = _lib()
-    g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
-    W = (torch.randn(N, K, generator=g) * 0.02).to(gpu_device, torch.bfloat16)
-    b = torch.randn(N, generator=g).to(gpu_device, torch.bfloat16)
-    ref = A.float() @ W.float().t()
-    C = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
-    rc = ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, ff.ptr(b), EPI_STORE, 14,
-                                      ff.stream_ptr())
-    if rc != 0:
-        assert b"contributor" in ff.lib().acehip_last_error()
-        pytest.skip("split needs two contributors per tile: refused")
-    torch.cuda.synchronize()
-    assert rel_l2(C.float().cpu(), (ref + b.float()).cpu()) < 5e-3
-    C1 = C.clone()
-    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), N, M, N, K, ff.ptr(b), EPI_STORE, 14,
-                                          ff.stream_ptr()))
-    torch.cuda.synchronize()
-    assert torch.equal(C, C1)                                    # deterministic, flags reset
-    R = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
-    C2 = R.clone()
-    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C2), N, M, N, K, None, EPI_RES, 14,
-                                          ff.stream_ptr()))
-    torch.cuda.synchronize()
-    assert rel_l2(C2.float().cpu(), (R.float() + ref.bfloat16().float()).cpu()) < 5e-3
-    if N % 64 == 0 and N >= 512:
-        Cs = torch.empty(M, N // 2, device=gpu_device, dtype=torch.bfloat16)
-        ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cs), N // 2, M, N, K, None,
-                                              EPI_SWIGLU, 14, ff.stream_ptr()))
-        torch.cuda.synchronize()
-        y = ref.bfloat16().float().view(M, N // 64, 2, 32)
-        gate, up = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
-        assert rel_l2(Cs.float().cpu(), (torch.nn.functional.silu(gate).bfloat16().float() * up).cpu()) < 1e-2
-    Cp = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
-    ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(Cp), N, M, N, K, ff.ptr(b), EPI_STORE,
-                                          -1, ff.stream_ptr()))
-    torch.cuda.synchronize()
-    assert rel_l2(Cp.float().cpu(), C.float().cpu()) < 5e-3
 
 
 def test_forward_graph_replay_matches_eager(gpu_device):
@@ -715,7 +642,7 @@ def test_gemm_small_m_paths(gpu_device, monkeypatch, M, N, K, epi):
         knobs = [{}, {"ACEHIP_SPLITK_BN": "64"}, {"ACEHIP_SPLITK_BN": "128"}]
     for kn in knobs:
         for k, v in kn.items():
-            monkeypatch.setenv(k, v)
+            set_knob(monkeypatch, k, v)
         C = C0.clone()
         ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), ncol, M, N, K, None, epi, -1,
                                               ff.stream_ptr()))
@@ -726,6 +653,7 @@ def test_gemm_small_m_paths(gpu_device, monkeypatch, M, N, K, epi):
         assert err < tol, (kn, err)
         for k in kn:
             monkeypatch.delenv(k)
+        ff.reload_knobs()
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(6000, 12288, 2048, EPI_SWIGLU), (15000, 12288, 2048, EPI_SWIGLU),
@@ -741,7 +669,7 @@ def test_gemm_tail_split(gpu_device, monkeypatch, M, N, K, epi):
     ncol = N // 2 if epi == EPI_SWIGLU else N
 
     def run(split):
-        monkeypatch.setenv("ACEHIP_GEMM_TAILSPLIT", "1" if split else "0")
+        set_knob(monkeypatch, "ACEHIP_GEMM_TAILSPLIT", "1" if split else "0")
         C = torch.full((M, ncol), float("nan"), device=gpu_device, dtype=torch.bfloat16)
         ff.check(ff.lib().acehip_gemm_bf16_ex(ff.ptr(A), K, ff.ptr(W), K, ff.ptr(C), ncol, M, N, K, None, epi, -1,
                                               ff.stream_ptr()))
@@ -776,16 +704,16 @@ def test_cfg_row_dedup_matches_full(gpu_device, monkeypatch):
     enc = torch.randn(2, 50, cfg.hidden_size, generator=g).bfloat16().to(gpu_device)
     rt.set_condition(enc)
     t = torch.tensor([0.7], dtype=torch.float32, device=gpu_device)
-    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
+    set_knob(monkeypatch, "ACEHIP_DIT_DEDUP", "0")
     full = rt.forward(xt, ctx, t).float().clone()
-    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "1")
+    set_knob(monkeypatch, "ACEHIP_DIT_DEDUP", "1")
     dd = rt.forward(xt, ctx, t).float()
     torch.cuda.synchronize()
     assert rel_l2(dd.cpu(), full.cpu()) < 2e-3
     # a per-row t (t_stride 1) must not take the shortcut: rows then differ
     t2 = torch.tensor([0.7, 0.3], dtype=torch.float32, device=gpu_device)
     a = rt.forward(xt, ctx, t2).float()
-    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
+    set_knob(monkeypatch, "ACEHIP_DIT_DEDUP", "0")
     b = rt.forward(xt, ctx, t2).float()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
@@ -815,8 +743,8 @@ def test_production_cfg_path_all_shortcuts(gpu_device, monkeypatch):
     x_d, c_d, t_d = xt.to(gpu_device), ctx.to(gpu_device), t.float().to(gpu_device)
     rt.set_uniform_rows(1)
     fast = rt.forward(x_d, c_d, t_d).float().clone()
-    monkeypatch.setenv("ACEHIP_DIT_DEDUP", "0")
-    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "0")
+    set_knob(monkeypatch, "ACEHIP_DIT_DEDUP", "0")
+    set_knob(monkeypatch, "ACEHIP_FUSE_ROWADD", "0")
     rt.set_uniform_rows(2)                                  # off: full cross-attention for every row
     full = rt.forward(x_d, c_d, t_d).float()
     torch.cuda.synchronize()
@@ -846,9 +774,9 @@ def test_null_row_add_fused_into_norm(gpu_device, monkeypatch):
     rt.set_condition(torch.cat([enc, null.expand_as(enc)]).to(gpu_device))
     rt.set_uniform_rows(B)
     t = torch.tensor([0.4], dtype=torch.float32, device=gpu_device)
-    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "0")
+    set_knob(monkeypatch, "ACEHIP_FUSE_ROWADD", "0")
     sep = rt.forward(xt, ctx, t).clone()
-    monkeypatch.setenv("ACEHIP_FUSE_ROWADD", "1")
+    set_knob(monkeypatch, "ACEHIP_FUSE_ROWADD", "1")
     fused = rt.forward(xt, ctx, t)
     torch.cuda.synchronize()
     assert torch.equal(sep, fused)
@@ -881,40 +809,6 @@ def test_forward_step_matches_forward(gpu_device, graph):
         assert torch.equal(a, b), i
     with pytest.raises(RuntimeError):
         rt.forward_step(xt, ctx, n)                  # outside the schedule
-    rt.close()
-
-
-def test_blaslt_projections(gpu_device, monkeypatch):
-    """ACEHIP_BLASLT (opt-in): hipBLASLt for the large-M QKV (+ standalone head_post), self-O /
-    down (AdaLN gate as the per-channel alpha vector, beta = 1 in place) and cross-O (beta = 1)
-    projections.  One fp32 rounding of gate * acc + x instead of the bf16 product then bf16 sum,
-    so within tolerance of the hand-written path, not bit-equal; the real width (D = 2048,
-    GQA 16 / 8, M = 2 x 600 rows > 256) through forward_step (one gate row for every batch row)."""
-    from acehip.dit import DiTRuntime
-    cfg = DiTConfig(hidden_size=2048, intermediate_size=4096, num_hidden_layers=2, num_attention_heads=16,
-                    num_key_value_heads=8, head_dim=128, sliding_window=128)
-    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=5, mode="parity").items()}
-    g = torch.Generator().manual_seed(3)
-    rt = DiTRuntime(cfg, 0, max_S=600, max_Bc=2, max_Lenc=64)
-    rt.load(W)
-    xt = torch.randn(2, 1200, 64, generator=g).bfloat16().to(gpu_device)
-    ctx = torch.randn(2, 1200, 128, generator=g).bfloat16().to(gpu_device)
-    rt.set_condition(torch.randn(2, 40, cfg.hidden_size, generator=g).bfloat16().to(gpu_device))
-    rt.set_timesteps(torch.tensor([0.7, 0.3], device=gpu_device))
-    outs = {}
-    for m in ("0", "7", "1", "2", "4"):
-        monkeypatch.setenv("ACEHIP_BLASLT", m)
-        outs[m] = rt.forward_step(xt, ctx, 1).float().clone()
-    torch.cuda.synchronize()
-    assert torch.isfinite(outs["7"]).all()
-    for m in ("7", "1", "2", "4"):
-        assert rel_l2(outs[m].cpu(), outs["0"].cpu()) < 1e-2, m      # two bf16 chains (oracle bar: 0.025)
-    assert not torch.equal(outs["2"], outs["0"])            # the hipBLASLt path actually ran
-    # forward(t[i]) (one broadcast t) takes the same paths as forward_step(i): bit-identical
-    monkeypatch.setenv("ACEHIP_BLASLT", "2")
-    a = rt.forward(xt, ctx, torch.tensor([0.3], device=gpu_device)).float()
-    torch.cuda.synchronize()
-    assert torch.equal(a, outs["2"])
     rt.close()
 
 
@@ -954,9 +848,9 @@ def test_splitk_epilogue_fused_into_consumers(gpu_device, monkeypatch, mode):
         rt.set_uniform_rows(0)
     t = torch.tensor([0.6], dtype=torch.float32, device=gpu_device)
     x_d, c_d = xt.to(gpu_device), ctx.to(gpu_device)
-    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "0")
+    set_knob(monkeypatch, "ACEHIP_SPLITK_FUSE", "0")
     sep = rt.forward(x_d, c_d, t).clone()
-    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "1")
+    set_knob(monkeypatch, "ACEHIP_SPLITK_FUSE", "1")
     fused = rt.forward(x_d, c_d, t)
     torch.cuda.synchronize()
     assert torch.equal(sep, fused)

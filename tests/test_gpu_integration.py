@@ -307,11 +307,16 @@ def test_install_drives_handler_calls(gpu_device, installed):
     n = T * 1920 + 777
     g = torch.Generator(device=gpu_device).manual_seed(11)
     audio = (0.3 * torch.randn(2, 2, n, device=gpu_device, generator=g)).float()
+    # placement (vae_encode.py:62-68): a source of <= chunk_size samples stays on the device even
+    # with the reference default offload_latent_to_cpu=True; a longer one is offloaded
     torch.manual_seed(5)
-    zc = h.tiled_encode(audio)                                  # reference default: offload
-    assert zc.device.type == "cpu" and zc.shape == (2, 64, T) and zc.dtype == torch.bfloat16
+    zs = h.tiled_encode(audio)
+    assert zs.is_cuda and zs.shape == (2, 64, T) and zs.dtype == torch.bfloat16
     torch.manual_seed(5)
-    zg = h.tiled_encode(audio, offload_latent_to_cpu=False)
+    zc = h.tiled_encode(audio, chunk_size=n - 1)                # "long" source: offloaded
+    assert zc.device.type == "cpu" and torch.equal(zc, zs.cpu())
+    torch.manual_seed(5)
+    zg = h.tiled_encode(audio, chunk_size=n - 1, offload_latent_to_cpu=False)
     assert zg.is_cuda and torch.equal(zg.cpu(), zc)
     torch.manual_seed(5)
     eps = torch.randn(2, 64, T, device=gpu_device, dtype=torch.bfloat16)

@@ -43,8 +43,11 @@ def dit2(gpu_device):
     return cfg, Wd, null
 
 
-@pytest.mark.parametrize("T", [6000, 15000])
-def test_dit_forward_full_length_cfg(gpu_device, dit2, T):
+@pytest.mark.parametrize("T,step", [(6000, False), (6000, True), (15000, False)])
+def test_dit_forward_full_length_cfg(gpu_device, dit2, T, step):
+    """The production call at real width: Bx = 1, Bc = 2 (CFG), one timestep for both rows,
+    null rows in closed form, layer-0 dedup; step=True goes through the sampler's own entry
+    (set_timesteps over a schedule + forward_step, base:1929-1941) — per row vs the oracle."""
     from acehip.dit import DiTRuntime
     cfg, W, null = dit2
     S, Lenc = (T + 1) // 2, 641
@@ -59,7 +62,12 @@ def test_dit_forward_full_length_cfg(gpu_device, dit2, T):
     rt.load(W)
     rt.set_condition(enc2)
     rt.set_uniform_rows(1)                         # CFG null rows in closed form (production)
-    out = rt.forward(xt, ctx, t).float()
+    if step:
+        sched = torch.tensor([1.0, 0.875, float(t), 0.25], dtype=torch.float32, device=gpu_device)
+        rt.set_timesteps(sched)
+        out = rt.forward_step(xt, ctx, 2).float()
+    else:
+        out = rt.forward(xt, ctx, t).float()
     torch.cuda.synchronize()
     rt.close()
     with torch.no_grad():

@@ -8,7 +8,7 @@ import pytest
 import torch
 from safetensors import safe_open
 
-from conftest import GOLDEN, cosine, load_golden, rel_l2
+from conftest import set_knob, GOLDEN, cosine, load_golden, rel_l2
 
 from acehip.config import DiTConfig
 from acehip.weights import synth_text_encoder_weights
@@ -73,9 +73,9 @@ def test_text_encoder_real_width_splitk_fusion(gpu_device, monkeypatch):
     te = TextEncoder(cfg, device=gpu_device.index or 0, max_batch=1, max_tokens=256)
     te.load({k: v.to(gpu_device) for k, v in W.items()})
     ids = torch.randint(0, 300, (1, 128), generator=torch.Generator().manual_seed(9)).to(gpu_device)
-    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "0")
+    set_knob(monkeypatch, "ACEHIP_SPLITK_FUSE", "0")
     sep = te(input_ids=ids).last_hidden_state.clone()
-    monkeypatch.setenv("ACEHIP_SPLITK_FUSE", "1")
+    set_knob(monkeypatch, "ACEHIP_SPLITK_FUSE", "1")
     fused = te(input_ids=ids).last_hidden_state
     torch.cuda.synchronize()
     assert torch.equal(sep, fused)
