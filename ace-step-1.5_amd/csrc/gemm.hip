@@ -35,6 +35,31 @@ namespace {
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 
+// GEMM_STAMPS (diagnostic builds only, tools/gemm_stamps.py): per workgroup and wave group,
+// shader-clock stamps at kernel entry, after the prologue, after the main loop and after the
+// epilogue, plus the real-time clock and the XCC id — where a tile's time goes
+#ifdef GEMM_STAMPS
+constexpr int STAMP_WG = 16384;
+__device__ unsigned long long g_gemm_stamps[STAMP_WG * 2 * 8];
+__device__ __forceinline__ void stamp(int slot, int i, unsigned long long v) {
+    if (slot < STAMP_WG * 2) {
+        asm volatile("" : "+v"(v));
+        g_gemm_stamps[slot * 8 + i] = v;
+    }
+}
+#define GSTAMP(i)                                                                                \
+    do {                                                                                         \
+        if ((threadIdx.x & 255) == 0) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memtime()); \
+    } while (0)
+#define GSTAMP_REAL(i)                                                                           \
+    do {                                                                                         \
+        if ((threadIdx.x & 255) == 0) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#else
+#define GSTAMP(i) do {} while (0)
+#define GSTAMP_REAL(i) do {} while (0)
+#endif
+
 // launch-attached timing events (gemm_ext_events): a hipEventRecord around a launch is its own
 // barrier packet — ≈ 5.6 µs of idle GPU before and after the timed kernel on this stack
 // (turbo timeline, tools/timeline.py) — while hipExtLaunchKernel stamps the dispatch itself
@@ -399,6 +424,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     static_assert(SM % 2 == 0, "A half must be whole 16-row sub-tiles");
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
 
+    GSTAMP(0);
+    GSTAMP_REAL(4);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
     const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
@@ -410,6 +437,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     const int tm = first_m + (wg % per_group) % gsz;
     const int tn = (wg % per_group) / gsz;
     const int m0 = tm * BM, n0 = tn * BN;
+#ifdef GEMM_STAMPS
+    {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if ((threadIdx.x & 255) == 0) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), 6, ((unsigned long long)wg << 32) | xcc);
+    }
+#endif
 
     const bf16_t *srcA[NA], *srcB[NB];
 #pragma unroll
@@ -474,6 +508,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
     bar();
     if (wr == 1) bar();   // group 1 runs one barrier behind
+    GSTAMP(1);
 
     constexpr int SCHED = BM == 256 ? 1 : 0;
     static_assert(SPL == 0 || SCHED == 1 || (SCHED == 0 && SPL == 1), "LDS-DMA spread: SCHED 1, or SPL 1 on SCHED 0");
@@ -613,6 +648,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
     }
     if (wr == 0) bar();   // balance the barrier count
+    GSTAMP(2);
 
     if constexpr (EPI == EPI_HEADPOST) {
         headpost_epilogue<BM, 8, sizeof(lds), 2>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
@@ -628,6 +664,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
 
     epilogue_tile<SM, 4, EPI>(a, acc, m0 + arow, n0 + wc * 64, fr, fc);
+#ifdef GEMM_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    GSTAMP(3);
+    GSTAMP_REAL(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -653,6 +694,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     static_assert(ROWS % 32 == 0, "staging must split evenly over 4 waves");
     __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
 
+    GSTAMP(0);
+    GSTAMP_REAL(4);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
@@ -737,6 +780,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    GSTAMP(1);
     rd(lds, 0, x0, w0);
     // refill pieces: one after every EVERY-th MFMA of half B, from MFMA FIRST on
     constexpr int EVERY = SM * SN / PW, FIRST = 1;
@@ -757,6 +801,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the asm MFMAs are opaque to the hazard recognizer: let the last ones retire
     // before their accumulators are read
+    GSTAMP(2);
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     if constexpr (EPI == EPI_HEADPOST) {
         headpost_epilogue<BM, 4, sizeof(lds), BN / 128>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
@@ -771,6 +816,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     } else {
         epilogue_tile<SM, SN, EPI>(a, acc, m0 + wm * TM, n0 + wn * TN, fr, fc);
     }
+#ifdef GEMM_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    GSTAMP(3);
+    GSTAMP_REAL(5);
 }
 
 template <int BM, int BN = 256>
@@ -838,11 +888,28 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 0: return launch<128, 128, 2, 2, 2>(a, s);   // 4 waves, 2-stage (2 blocks/CU): half-chip grids, tails
         case 7: return launch_pp<256>(a, s);              // ping-pong 256x256 (128 KiB)
         case 8: return launch_pp<192>(a, s);              // ping-pong 192x256 (112 KiB)
+        case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
         case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
         default: return fail(-1, "gemm: bad variant (0, 7, 8, 13, 16)");
     }
 }
+
+#ifdef GEMM_STAMPS
+}  // namespace acehip
+extern "C" int acehip_diag_gemm_stamps(void *host, int n_wg) {
+    n_wg = std::min(n_wg, acehip::STAMP_WG);
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(acehip::g_gemm_stamps), (size_t)n_wg * 2 * 8 * 8));
+    return 0;
+}
+extern "C" int acehip_diag_gemm_stamps_clear(void) {
+    void *p = nullptr;
+    HIP_TRY(hipGetSymbolAddress(&p, HIP_SYMBOL(acehip::g_gemm_stamps)));
+    HIP_TRY(hipMemset(p, 0, sizeof(acehip::g_gemm_stamps)));
+    return 0;
+}
+namespace acehip {
+#endif
 
 bool gemm_ext_events(hipEvent_t start, hipEvent_t stop) {
     const bool consumed = g_ext_ev.stop && !g_ext_ev.start;

@@ -10,3 +10,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/${TAG}_smoke.log
 timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
+timeout -k 10 300 python -u tools/gemm_stamps.py > gpurun_out/${TAG}_stamps.log 2>&1 || { tail -20 gpurun_out/${TAG}_stamps.log; exit 1; }
+cat gpurun_out/${TAG}_stamps.log
+VARIANTS=7,8,11 ROUNDS=3 COLD=1 SHAPES=swiglu,down,qkv,o timeout -k 10 300 python -u tools/bench_gemm.py > gpurun_out/${TAG}_bench_gemm.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_gemm.log; exit 1; }
+cat gpurun_out/${TAG}_bench_gemm.log
