@@ -38,12 +38,27 @@ __host__ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 // round an fp32 value through bf16 (models one torch bf16 op's output rounding)
 __host__ __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+// rbf over an array, two values per v_cvt_pk_bf16_f32 (+ a shift and a mask to widen them
+// back): the same rounding as N calls of rbf, half the conversions
+template <int N>
+__device__ __forceinline__ void rbf_n(float *x) {
+    static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x[i], x[i + 1]}, bf16x2));
+        x[i] = __builtin_bit_cast(float, u << 16);
+        x[i + 1] = __builtin_bit_cast(float, u & 0xffff0000u);
+    }
+}
 // two fp32 → packed bf16 pair (low half = a)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// silu = x·σ(x) = x / (1 + e^−x); the reciprocal by v_rcp_f32 (1 ulp) instead of the IEEE
+// division sequence (div_scale ×2, rcp, 5 FMAs, div_fmas, div_fixup): the SwiGLU epilogue is
+// VALU-bound and the result is rounded to bf16 right after
+__device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // pack/unpack 8 bf16 in a uint4
 __device__ __forceinline__ void unpack8(const uint4 &u, float *f) {
@@ -71,11 +86,20 @@ __device__ __forceinline__ void unpack4(const uint2 &u, float *f) {
 // at offset 8·(fc >> 1): one 4-value swap with lane ^ 16.  Turns an epilogue's 8-B
 // accesses into 16-B ones (the store tail is issue-bound).
 __device__ __forceinline__ void pair8(const f32x4 &lo, const f32x4 &hi, bool odd, float (&v)[8]) {
+    // v_permlane16_swap_b32 (VALU, no LDS round trip): the odd 16-lane rows of its first operand
+    // trade with the even rows of its second — with (lo, hi) that hands the even rows their odd
+    // partner's lo and the odd rows their even partner's hi, so v = (first, second) in every
+    // lane.  Both lanes of a pair must be active.  Inline asm: ROCm 7.2's
+    // __builtin_amdgcn_permlane16_swap folds the four calls into the first one's result
+    // (every r got r = 0's values); the s_nop 1 is the VALU-write → permlane-read wait the
+    // compiler does not insert for asm.
+    (void)odd;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const float got = __shfl_xor(odd ? lo[r] : hi[r], 16, 64);
-        v[r] = odd ? got : lo[r];
-        v[4 + r] = odd ? hi[r] : got;
+        float a = lo[r], b = hi[r];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+        v[r] = a;
+        v[4 + r] = b;
     }
 }
 

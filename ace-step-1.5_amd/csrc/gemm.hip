@@ -112,10 +112,24 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                 // silu(gate)·up in the MFMA layout first, then one exchange of the products
                 f32x4 p0, p1;
                 float o[8];
+                // bf16(gate) and bf16(up) of both sub-tiles, pairwise rounded, then silu
+                float g8[8], u8[8];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    p0[r] = rbf(silu_f(rbf(acc[i][4 * pnl][r]))) * rbf(acc[i][4 * pnl + 2][r]);
-                    p1[r] = rbf(silu_f(rbf(acc[i][4 * pnl + 1][r]))) * rbf(acc[i][4 * pnl + 3][r]);
+                    g8[r] = acc[i][4 * pnl][r];
+                    g8[4 + r] = acc[i][4 * pnl + 1][r];
+                    u8[r] = acc[i][4 * pnl + 2][r];
+                    u8[4 + r] = acc[i][4 * pnl + 3][r];
+                }
+                rbf_n<8>(g8);
+                rbf_n<8>(u8);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) g8[r] = silu_f(g8[r]);
+                rbf_n<8>(g8);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    p0[r] = g8[r] * u8[r];
+                    p1[r] = g8[4 + r] * u8[4 + r];
                 }
                 pair8(p0, p1, odd, o);
                 const int nout = ((col0 + pnl * 64) >> 1) + (odd ? 16 : 0) + cpos;
@@ -170,15 +184,17 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                     } else {
                         float rr[8];
                         unpack8(rv[ii][jp], rr);
+                        // same roundings as rr + bf16(bf16(o)·g) / rr + bf16(o), pairwise
+                        rbf_n<8>(o);
                         if constexpr (EPI == EPI_GATED_RES) {
                             float gg[8];
                             unpack8(gv[ii][jp], gg);
 #pragma unroll
-                            for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(rbf(o[r]) * gg[r]);
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 8; ++r) o[r] = rr[r] + rbf(o[r]);
+                            for (int r = 0; r < 8; ++r) o[r] *= gg[r];
+                            rbf_n<8>(o);
                         }
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) o[r] = rr[r] + o[r];
                     }
                     if (live) *(uint4 *)(a.C + (int64_t)m * a.ldc + n) = pack8(o);
                 }

@@ -32,10 +32,15 @@ __device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm,
     ss += row_ror<4>(ss);
     ss += row_ror<2>(ss);
     ss += row_ror<1>(ss);
+    // (bf16 roundings two at a time, rbf_n: the same values as per-element rbf)
     if (norm) {
         const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + eps);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = rbf(w[j] * rbf(x[j] * r));
+        for (int j = 0; j < 8; ++j) x[j] *= r;
+        rbf_n<8>(x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] *= w[j];
+        rbf_n<8>(x);
     }
     if (rope) {
         float p[8];
@@ -44,7 +49,14 @@ __device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm,
         if (norm) {
             const float sg = li < 8 ? -1.0f : 1.0f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = rbf(x[j] * cs[j]) + rbf(sg * p[j] * sn[j]);
+            for (int j = 0; j < 8; ++j) {
+                x[j] *= cs[j];
+                p[j] = sg * p[j] * sn[j];
+            }
+            rbf_n<8>(x);
+            rbf_n<8>(p);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] += p[j];
         }
     }
 }
