@@ -19,7 +19,7 @@ from acehip import _ffi as ff  # noqa: E402
 dev = torch.device("cuda:0")
 # name: (M, N, K, epi, variant)  — epi 0 store, 3 SwiGLU; variants as the cost model picks them
 SHAPES = {"swiglu": (6000, 12288, 2048, 3, 7), "down": (6000, 2048, 6144, 2, 8), "qkv": (6000, 4096, 2048, 0, 8),
-          "o": (6000, 2048, 2048, 2, 8), "o_half": (3000, 2048, 2048, 2, 0)}
+          "o": (6000, 2048, 2048, 2, 8), "o_half": (3000, 2048, 2048, 2, 13), "crossq": (3000, 2048, 2048, 0, 13)}
 
 
 def load(path):
@@ -37,6 +37,8 @@ libs = [load(None)] + [load(p) for p in sys.argv[1:]]
 # AB_VARIANT forces one variant for every shape (A/B of a kernel's schedule builds)
 if os.environ.get("AB_VARIANT"):
     SHAPES = {k: v[:4] + (int(os.environ["AB_VARIANT"]),) for k, v in SHAPES.items()}
+# AB_VARIANTS=v1,v2,...: every listed variant of the working-tree library as its own arm
+EXTRA_VARIANTS = [int(v) for v in os.environ.get("AB_VARIANTS", "").split(",") if v]
 if os.environ.get("SHAPES"):
     SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 res = {}
@@ -48,32 +50,35 @@ for name, (M, N, K, epi, var) in SHAPES.items():
     Ws = [((torch.rand(N, K, device=dev, generator=g) * 2 - 1) * 0.05).bfloat16() for _ in range(min(nrot, 4))]
     Ws += [Ws[i % len(Ws)].clone() for i in range(nrot - len(Ws))]
     ldc = N // 2 if epi == 3 else N
+    # arms: (label, entry point, variant) — every library at the shape's variant, plus the
+    # working tree's AB_VARIANTS
+    arms = [(ln, f, var) for ln, f in libs] + [(f"tree_v{v}", libs[0][1], v) for v in EXTRA_VARIANTS]
     outs = {}
-    times = {ln: [] for ln, _ in libs}
+    times = {ln: [] for ln, _, _ in arms}
     rot = [0]
 
-    def run(f, C):
+    def run(f, v, C):
         W = Ws[rot[0] % nrot]
         rot[0] += 1
-        assert f(A.data_ptr(), K, W.data_ptr(), K, C.data_ptr(), ldc, M, N, K, None, epi, var,
+        assert f(A.data_ptr(), K, W.data_ptr(), K, C.data_ptr(), ldc, M, N, K, None, epi, v,
                  ff.stream_ptr().value) == 0
 
-    for ln, f in libs:
-        C = torch.empty(M, ldc, device=dev, dtype=torch.bfloat16)
+    for ln, f, v in arms:
+        C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)   # the residual of epi 2
         rot[0] = 0
-        run(f, C)
+        run(f, v, C)
         torch.cuda.synchronize()
         outs[ln] = C.float()
     for _ in range(5):
-        for ln, f in libs:
-            C = torch.empty(M, ldc, device=dev, dtype=torch.bfloat16)
+        for ln, f, v in arms:
+            C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
             for _ in range(3):
-                run(f, C)
+                run(f, v, C)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             n = 20
             e0.record()
             for _ in range(n):
-                run(f, C)
+                run(f, v, C)
             e1.record()
             torch.cuda.synchronize()
             times[ln].append(e0.elapsed_time(e1) / n * 1e3)

@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+SHAPES=swiglu,down,o,down256,qkv timeout -k 10 300 python -u tools/gemm_stamps.py > gpurun_out/r04c_stamps.log 2>&1 || { tail -20 gpurun_out/r04c_stamps.log; exit 1; }
+cat gpurun_out/r04c_stamps.log
