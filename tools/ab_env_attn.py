@@ -11,6 +11,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
 import torch  # noqa: E402
+from acehip._ffi import reload_knobs  # noqa: E402  (the library reads its switches once)
 from acehip import _ffi as ff  # noqa: E402
 
 dev = torch.device("cuda:0")
@@ -36,14 +37,17 @@ for name, (B, H, KV, Sq, Sk, w) in SHAPES.items():
     outs = []
     for i, st in enumerate(settings):
         os.environ.update(st)
+        reload_knobs()
         call(q, k, v, o, B, H, KV, Sq, Sk, w)
         torch.cuda.synchronize()
         outs.append(o.float().clone())
         for kk in st:
             os.environ.pop(kk)
+            reload_knobs()
     for _ in range(7):
         for i, st in enumerate(settings):
             os.environ.update(st)
+            reload_knobs()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
@@ -53,6 +57,7 @@ for name, (B, H, KV, Sq, Sk, w) in SHAPES.items():
             times[i].append(e0.elapsed_time(e1) / 10 * 1e3)
             for kk in st:
                 os.environ.pop(kk)
+                reload_knobs()
     row = []
     for i, st in enumerate(settings):
         rel = float((outs[i] - outs[0]).norm() / outs[0].norm())

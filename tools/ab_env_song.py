@@ -12,6 +12,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
 import torch  # noqa: E402
+from acehip._ffi import reload_knobs  # noqa: E402  (the library reads its switches once)
 from acehip.config import DiTConfig  # noqa: E402
 from acehip.dit import AceStepDiTBackend, DiTRuntime  # noqa: E402
 from acehip.weights import synth_dit_weights  # noqa: E402
@@ -44,12 +45,15 @@ def song():
 outs, times = [], [[] for _ in settings]
 for st in settings:
     os.environ.update(st)
+    reload_knobs()
     outs.append(song().float().clone())
     for k in st:
         os.environ.pop(k)
+        reload_knobs()
 for _ in range(int(os.environ.get("ROUNDS", "3"))):
     for i, st in enumerate(settings):
         os.environ.update(st)
+        reload_knobs()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         song()
@@ -57,6 +61,7 @@ for _ in range(int(os.environ.get("ROUNDS", "3"))):
         times[i].append((time.perf_counter() - t0) * 1e3)
         for k in st:
             os.environ.pop(k)
+            reload_knobs()
 for i, st in enumerate(settings):
     same = torch.equal(outs[i], outs[0])
     print(f"{','.join(f'{a}={b}' for a, b in st.items()) or 'default'}: DiT song {statistics.median(times[i]):.1f} ms "

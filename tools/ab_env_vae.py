@@ -11,6 +11,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "ace-step-1.5_amd")]
 import torch  # noqa: E402
+from acehip._ffi import reload_knobs  # noqa: E402  (the library reads its switches once)
 from acehip.config import VAEConfig  # noqa: E402
 from acehip.vae import OobleckBackend  # noqa: E402
 from acehip.weights import synth_vae_weights  # noqa: E402
@@ -27,12 +28,15 @@ z = torch.randn(1, 64, T, device=dev, generator=g).bfloat16()
 outs, times = [], [[] for _ in settings]
 for st in settings:
     os.environ.update(st)
+    reload_knobs()
     outs.append(vae.decode_tensor(z).float().clone())
     for k in st:
         os.environ.pop(k)
+        reload_knobs()
 for _ in range(5):
     for i, st in enumerate(settings):
         os.environ.update(st)
+        reload_knobs()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         vae.decode_tensor(z)
@@ -40,6 +44,7 @@ for _ in range(5):
         times[i].append((time.perf_counter() - t0) * 1e3)
         for k in st:
             os.environ.pop(k)
+            reload_knobs()
 for i, st in enumerate(settings):
     print(f"{','.join(f'{a}={b}' for a, b in st.items()) or 'default'}: decode {statistics.median(times[i]):.2f} ms "
           f"(min {min(times[i]):.2f}; bit-identical to baseline: {torch.equal(outs[i], outs[0])})", flush=True)
