@@ -432,7 +432,10 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
 //      (the ablation behind it: without the main-loop DMA the 256² tile ran 22 % faster,
 //      without the fragment reads 18 %, without both 37 %)
 // SCHED 0 takes SPL 1 only: A(kt+1) split between phases 0 and 1 (phase 3 has no reads)
-template <int BM, int EPI, int SPL = (BM == 256 ? 3 : 0)>
+// SCHED 2: two phases per K-tile, each over both k-steps (half the barriers; 24 / 32 MFMAs
+// per interval at 192 / 256 rows): phase 0 reads all four B sub-tiles and A-half 0 and
+// stages A(kt+1), phase 1 reads A-half 1 and stages B(kt+2); reads retire before each barrier
+template <int BM, int EPI, int SPL = (BM == 256 ? 3 : 0), int SCHED = (BM == 256 ? 1 : 0)>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
     constexpr int ROWS = BM + BN, BUF = ROWS * 128;
@@ -526,9 +529,56 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     if (wr == 1) bar();   // group 1 runs one barrier behind
     GSTAMP(1);
 
-    constexpr int SCHED = BM == 256 ? 1 : 0;
-    static_assert(SPL == 0 || SCHED == 1 || (SCHED == 0 && SPL == 1), "LDS-DMA spread: SCHED 1, or SPL 1 on SCHED 0");
-    if constexpr (SCHED == 1) {
+    static_assert(SCHED == 2 || SPL == 0 || SCHED == 1 || (SCHED == 0 && SPL == 1),
+                  "LDS-DMA spread: SCHED 1, or SPL 1 on SCHED 0");
+    if constexpr (SCHED == 2) {
+    bf16x8 xa[SMH][2], bf[4][2];
+    auto readA = [&](const char *b, int h) {
+#pragma unroll
+        for (int i = 0; i < SMH; ++i)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+                xa[i][ks] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
+    };
+    auto mma = [&](int h) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < SMH; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[h * SMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], xa[i][ks], acc[h * SMH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+        const char *b = lds + (kt & 1) * BUF;
+        // phase 0: B (all four sub-tiles, both k-steps) + A-half 0; A(kt+1) → other buffer
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) bf[j][ks] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
+        readA(b, 0);
+        if (kt + 1 < nk) stageA((kt + 1) & 1, (kt + 1) * BK);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        mma(0);
+        bar();
+        // phase 1: A-half 1; B(kt+2) → this buffer's B slots (tile kt's B: last read by the
+        // other group in its phase 0, retired before the barrier above), then A(kt+1) landed
+        readA(b, 1);
+        if (kt + 2 < nk) {
+            stageB(kt & 1, (kt + 2) * BK);
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        bar();
+        mma(1);
+        bar();
+    }
+    } else if constexpr (SCHED == 1) {
     // Balanced schedule: phase p multiplies A-half (p & 1) by all four B sub-tiles at
     // k-step (p >> 1), so a loader wave issues 8, 4, 8, 4 ds_read_b128 per phase (the
     // 12-read first phase of the schedule below, plus the A(kt+1) DMA, saturates the
@@ -860,18 +910,19 @@ int launch_w4(const GemmArgs &a, hipStream_t s) {
     return 0;
 }
 
-template <int BM>
+template <int BM, int SCHED = (BM == 256 ? 1 : 0)>
 int launch_pp(const GemmArgs &a, hipStream_t s) {
     if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
     const int tiles = ((a.M + BM - 1) / BM) * (a.N / 256);
+    constexpr int SP = SCHED == 2 ? 0 : (BM == 256 ? 3 : 0);
     switch (a.epi) {
-        case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
+        case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_RES: gemm_pp_kernel<BM, EPI_RES, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU, SP, SCHED>, dim3(tiles), dim3(512), s, a); break;
         case EPI_HEADPOST:
             if constexpr (BM == 192 || BM == 128) {
-                gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
+                gemm_pp_kernel<BM, EPI_HEADPOST, SP, SCHED><<<tiles, 512, 0, s>>>(a);
                 break;
             }
             return fail(-1, "gemm: head-post epilogue needs the 192- or 128-row ping-pong tile");
@@ -902,12 +953,14 @@ int launch(const GemmArgs &a, hipStream_t s) {
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
     switch (variant) {
         case 0: return launch<128, 128, 2, 2, 2>(a, s);   // 4 waves, 2-stage (2 blocks/CU): half-chip grids, tails
-        case 7: return launch_pp<256>(a, s);              // ping-pong 256x256 (128 KiB)
-        case 8: return launch_pp<192>(a, s);              // ping-pong 192x256 (112 KiB)
+        // ping-pong 256x256 (128 KiB) / 192x256 (112 KiB): two phases per K-tile
+        // (ACEHIP_GEMM_PPSCHED=1: the four-phase schedules, A/B)
+        case 7: return knobs().gemm_ppsched == 2 ? launch_pp<256, 2>(a, s) : launch_pp<256, 1>(a, s);
+        case 8: return knobs().gemm_ppsched == 2 ? launch_pp<192, 2>(a, s) : launch_pp<192, 0>(a, s);
         case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
         case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
-        default: return fail(-1, "gemm: bad variant (0, 7, 8, 13, 16)");
+        default: return fail(-1, "gemm: bad variant (0, 7, 8, 11, 13, 16)");
     }
 }
 
@@ -1138,7 +1191,7 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
             hh.ld_src = a.N;
             return head_post(hh, s);
         }
-        return launch_pp<192>(a, s);
+        return gemm_variant(a, 8, s);
     }
     const int v = gemm_pick_variant(a.M, a.N);
     if (v == 7 || v == 8) {

@@ -50,6 +50,18 @@ EPI_STORE, EPI_GATED_RES, EPI_RES, EPI_SWIGLU = 0, 1, 2, 3
 def test_gemm_variants(gpu_device, variant, M, N, K):
     """Every production tile variant, odd K-tile counts (ring prologue/tail) and ragged M,
     plain store + SwiGLU epilogue (gate/up interleaved in 32-row panels)."""
+    _gemm_variant_check(gpu_device, variant, M, N, K)
+
+
+@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("M,N,K", [(517, 256, 128), (777, 768, 640)])
+def test_gemm_pingpong_four_phase(gpu_device, monkeypatch, variant, M, N, K):
+    """The four-phase ping-pong schedules (ACEHIP_GEMM_PPSCHED=1, the A/B arm)."""
+    set_knob(monkeypatch, "ACEHIP_GEMM_PPSCHED", "1")
+    _gemm_variant_check(gpu_device, variant, M, N, K)
+
+
+def _gemm_variant_check(gpu_device, variant, M, N, K):
     ff = _lib()
     if variant in (7, 8) and N % 256:
         pytest.skip("variant needs N % 256 == 0")
