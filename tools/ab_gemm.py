@@ -39,6 +39,24 @@ if os.environ.get("AB_VARIANT"):
     SHAPES = {k: v[:4] + (int(os.environ["AB_VARIANT"]),) for k, v in SHAPES.items()}
 # AB_VARIANTS=v1,v2,...: every listed variant of the working-tree library as its own arm
 EXTRA_VARIANTS = [int(v) for v in os.environ.get("AB_VARIANTS", "").split(",") if v]
+# AB_KNOBS=NAME=VAL;...: the working-tree library with one switch set, as its own arm (the
+# library reads its switches once: set + acehip_reload_knobs around that arm's launches)
+EXTRA_KNOBS = [kv for kv in os.environ.get("AB_KNOBS", "").split(";") if kv]
+
+
+def knob(label):
+    if label.startswith("tree_") and "=" in label:
+        k, v = label[5:].split("=", 1)
+        os.environ[k] = v
+        ff.reload_knobs()
+        return k
+    return None
+
+
+def unknob(k):
+    if k:
+        os.environ.pop(k)
+        ff.reload_knobs()
 if os.environ.get("SHAPES"):
     SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 res = {}
@@ -53,6 +71,7 @@ for name, (M, N, K, epi, var) in SHAPES.items():
     # arms: (label, entry point, variant) — every library at the shape's variant, plus the
     # working tree's AB_VARIANTS
     arms = [(ln, f, var) for ln, f in libs] + [(f"tree_v{v}", libs[0][1], v) for v in EXTRA_VARIANTS]
+    arms += [(f"tree_{kv}", libs[0][1], var) for kv in EXTRA_KNOBS]
     outs = {}
     times = {ln: [] for ln, _, _ in arms}
     rot = [0]
@@ -66,12 +85,15 @@ for name, (M, N, K, epi, var) in SHAPES.items():
     for ln, f, v in arms:
         C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)   # the residual of epi 2
         rot[0] = 0
+        kk = knob(ln)
         run(f, v, C)
         torch.cuda.synchronize()
+        unknob(kk)
         outs[ln] = C.float()
     for _ in range(5):
         for ln, f, v in arms:
             C = torch.zeros(M, ldc, device=dev, dtype=torch.bfloat16)
+            kk = knob(ln)
             for _ in range(3):
                 run(f, v, C)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -81,6 +103,7 @@ for name, (M, N, K, epi, var) in SHAPES.items():
                 run(f, v, C)
             e1.record()
             torch.cuda.synchronize()
+            unknob(kk)
             times[ln].append(e0.elapsed_time(e1) / n * 1e3)
     # hipBLASLt (torch.matmul, plain store, no epilogue) on the same box for reference
     Wts = [w.t() for w in Ws]
