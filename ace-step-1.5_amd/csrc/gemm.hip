@@ -347,9 +347,36 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a, int sp
 // store.  A lane's units: a fixed head (hh = sub & 1) and rows r = wave·2 + (sub >> 1)
 // + 2·NW·it, so (batch, position) advance incrementally (no integer division per unit)
 // and every cos/sin row is loaded BEFORE the first store (a load's vmcnt would
-// otherwise also wait for the older stores).
+// otherwise also wait for the older stores).  When both heads of every tile are of one
+// kind (q / k / v boundaries at even heads: the DiT's 16 | 8 | 8) the kind is a scalar, so
+// the norm / RoPE choice is a scalar branch; otherwise (tiny test layouts) per lane.
 //
 // HPT = 1: a BM×128 tile holds one head; the four 16-lane groups of a wave take four rows.
+template <int MODE, int ITER, int RPI, int PITCH>
+__device__ __forceinline__ void headpost_rows(const GemmArgs &a, const bf16_t *st, int m0, int r0, int hh, int li,
+                                              int d, int b0, int s0, bf16_t *base, int64_t bstride, bool norm,
+                                              const float (&w)[8], const uint4 (&cv)[ITER], const uint4 (&sv)[ITER]) {
+    // MODE: 0 v heads (scatter), 1 q/k without RoPE, 2 q/k with RoPE, 3 per-lane `norm`
+    const HeadPostArgs &h = a.hp;
+    int bq = b0, sq = s0;
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int r = r0 + RPI * it;
+        float x[8], cs[8] = {}, sn[8] = {};
+        unpack8(*(const uint4 *)(st + r * PITCH + hh * 128 + d), x);
+        if constexpr (MODE >= 2) {
+            unpack8(cv[it], cs);
+            unpack8(sv[it], sn);
+        }
+        if constexpr (MODE == 1) head_norm_rope_t<true, false>(x, li, w, cs, sn, h.eps);
+        else if constexpr (MODE == 2) head_norm_rope_t<true, true>(x, li, w, cs, sn, h.eps);
+        else if constexpr (MODE == 3) head_norm_rope(x, li, norm, w, h.cos != nullptr, cs, sn, h.eps);
+        if (m0 + r < a.M) *(uint4 *)(base + (int64_t)bq * bstride + sq * 128) = pack8(x);
+        sq += RPI;
+        while (sq >= h.S) { sq -= h.S; ++bq; }
+    }
+}
+
 template <int BM, int NW, int LDS_BYTES, int HPT, typename StoreAcc>
 __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, int m0, int n0, int wave, int lane,
                                                   StoreAcc store_acc) {
@@ -363,7 +390,8 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
     const HeadPostArgs &h = a.hp;
     const int sub = lane >> 4, li = lane & 15, d = li * 8, hh = HPT == 2 ? sub & 1 : 0;
     const int head = (n0 >> 7) + hh;
-    const bool norm = head < h.nq + h.nk;
+    const int nqk = h.nq + h.nk;
+    const bool norm = head < nqk;
     const bool rope = h.cos != nullptr;
     const int r0 = wave * RPW + (HPT == 2 ? sub >> 1 : sub);
     const int mf = min(m0 + r0, a.M - 1);
@@ -380,28 +408,37 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
             while (sq >= h.S) sq -= h.S;
         }
     }
+    // destination of this lane's head at (b = 0, s = 0) + its 8 columns, and the batch stride
+    bf16_t *base;
+    int64_t bstride;
+    const int64_t hs = (int64_t)h.S_dst * 128;
+    if (head < h.nq) {
+        base = h.q + head * hs;
+        bstride = h.nq * hs;
+    } else if (head < nqk) {
+        base = h.k + (head - h.nq) * hs;
+        bstride = h.nk * hs;
+    } else {
+        base = h.v + (head - nqk) * hs;
+        bstride = h.nv * hs;
+    }
+    base += d;
     float w[8] = {};
     if (norm) unpack8(*(const uint4 *)((head < h.nq ? h.qw : h.kw) + d), w);
     bf16_t *st = (bf16_t *)lds;
     __syncthreads();
     store_acc(st, PITCH);
     __syncthreads();
-    int bq = b0, sq = s0;
-#pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-        const int r = r0 + RPI * it;
-        float x[8], cs[8] = {}, sn[8] = {};
-        unpack8(*(const uint4 *)(st + r * PITCH + hh * 128 + d), x);
-        if (rope) {
-            unpack8(cv[it], cs);
-            unpack8(sv[it], sn);
-        }
-        const bf16_t *nw;
-        bf16_t *dst = head_dst(h, head, bq, sq, nw);
-        head_norm_rope(x, li, norm, w, rope, cs, sn, h.eps);
-        if (m0 + r < a.M && dst) *(uint4 *)(dst + d) = pack8(x);
-        sq += RPI;
-        while (sq >= h.S) { sq -= h.S; ++bq; }
+    const bool uniform = HPT == 1 || (h.nq % 2 == 0 && nqk % 2 == 0);
+    if (uniform) {
+        if ((n0 >> 7) >= nqk)
+            headpost_rows<0, ITER, RPI, PITCH>(a, st, m0, r0, hh, li, d, b0, s0, base, bstride, norm, w, cv, sv);
+        else if (!rope)
+            headpost_rows<1, ITER, RPI, PITCH>(a, st, m0, r0, hh, li, d, b0, s0, base, bstride, norm, w, cv, sv);
+        else
+            headpost_rows<2, ITER, RPI, PITCH>(a, st, m0, r0, hh, li, d, b0, s0, base, bstride, norm, w, cv, sv);
+    } else {
+        headpost_rows<3, ITER, RPI, PITCH>(a, st, m0, r0, hh, li, d, b0, s0, base, bstride, norm, w, cv, sv);
     }
 }
 

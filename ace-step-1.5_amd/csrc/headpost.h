@@ -22,42 +22,57 @@ __device__ __forceinline__ float row_ror(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xF, 0xF, false));
 }
 
-__device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm, const float (&w)[8], bool rope,
-                                               const float (&cs)[8], const float (&sn)[8], float eps) {
-    float ss = 0.f;
+// NORM: q / k head (RMSNorm, then RoPE when ROPE); a v head passes through unchanged.
+// rsqrt by v_rsq_f32 (the reference's torch.rsqrt; the IEEE 1/sqrtf expansion was ~35 VALU
+// per head row); the rotate-half sign folds into one fma: x·cos + sg·bf16(p·sin), sg·t exact
+template <bool NORM, bool ROPE>
+__device__ __forceinline__ void head_norm_rope_t(float (&x)[8], int li, const float (&w)[8], const float (&cs)[8],
+                                                 const float (&sn)[8], float eps) {
+    if constexpr (NORM) {
+        float ss = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
-    // all-reduce over the 16 lanes of the head: rotations by 8, 4, 2, 1 within the row
-    ss += row_ror<8>(ss);
-    ss += row_ror<4>(ss);
-    ss += row_ror<2>(ss);
-    ss += row_ror<1>(ss);
-    // (bf16 roundings two at a time, rbf_n: the same values as per-element rbf)
-    if (norm) {
-        const float r = 1.0f / sqrtf(ss * (1.0f / 128.0f) + eps);
+        for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+        // all-reduce over the 16 lanes of the head: rotations by 8, 4, 2, 1 within the row
+        ss += row_ror<8>(ss);
+        ss += row_ror<4>(ss);
+        ss += row_ror<2>(ss);
+        ss += row_ror<1>(ss);
+        // (bf16 roundings two at a time, rbf_n: the same values as per-element rbf)
+        const float r = __builtin_amdgcn_rsqf(ss * (1.0f / 128.0f) + eps);
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] *= r;
         rbf_n<8>(x);
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] *= w[j];
         rbf_n<8>(x);
-    }
-    if (rope) {
-        float p[8];
+        if constexpr (ROPE) {
+            float p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = row_ror<8>(x[j]);   // rotate-half partner d ± 64 (lane ^ 8)
-        if (norm) {
-            const float sg = li < 8 ? -1.0f : 1.0f;
+            for (int j = 0; j < 8; ++j) p[j] = row_ror<8>(x[j]) * sn[j];   // rotate-half partner d ± 64 (lane ^ 8)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                x[j] *= cs[j];
-                p[j] = sg * p[j] * sn[j];
-            }
+            for (int j = 0; j < 8; ++j) x[j] *= cs[j];
             rbf_n<8>(x);
             rbf_n<8>(p);
+            const float sg = li < 8 ? -1.0f : 1.0f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] += p[j];
+            for (int j = 0; j < 8; ++j) x[j] = __builtin_fmaf(sg, p[j], x[j]);
         }
+    }
+}
+
+// runtime-flag form (the standalone head_post kernel, mixed-type tiles): every lane of the wave
+// must call it (it shuffles); `rope` must be uniform over the wave
+__device__ __forceinline__ void head_norm_rope(float (&x)[8], int li, bool norm, const float (&w)[8], bool rope,
+                                               const float (&cs)[8], const float (&sn)[8], float eps) {
+    // the lane reductions run unmasked: a v head's lanes compute and discard
+    float y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = x[j];
+    if (rope) head_norm_rope_t<true, true>(y, li, w, cs, sn, eps);
+    else head_norm_rope_t<true, false>(y, li, w, cs, sn, eps);
+    if (norm) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = y[j];
     }
 }
 
