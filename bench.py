@@ -229,6 +229,7 @@ def main():
                                 synth_text_encoder_weights, synth_vae_weights)
     from acehip.condition import ConditionEncoder, HipPrepareCondition, TextEncoder
     from acehip.flops import dit_flops_executed_cfg_song_step, dit_flops_per_row, vae_decoder_flops
+    from acehip.provenance import product_hash
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -416,6 +417,8 @@ def main():
             roofline["pmc_from"] = {
                 "file": os.path.relpath(args.pmc_json, REPO), "same_run": False,
                 "box": pm.get("box"), "git_head": pm.get("git_head"),
+                "product_hash": pm.get("product_hash"),
+                "same_product_code": pm.get("product_hash") == product_hash(),
                 "clock_GHz": sw.get("clock_GHz"), "mfma_busy_frac": sw.get("mfma_busy_frac"),
                 "avg_us_in_pass": sw.get("avg_us"),
                 "note": "counter passes of the same kernel shape on the named box (separate runs); "

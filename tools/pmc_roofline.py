@@ -29,6 +29,14 @@ import sqlite3
 from collections import defaultdict
 
 
+def _product_hash():
+    import os as _os
+    import sys as _sys
+    _sys.path.insert(0, _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ace-step-1.5_amd"))
+    from acehip.provenance import product_hash
+    return product_hash()
+
+
 def _short(name):
     name = name.replace("acehip::(anonymous namespace)::", "").replace("void ", "")
     return re.sub(r"\(.*\)$", "", name)
@@ -120,7 +128,7 @@ def main():
           "per_kind": per_kind}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES,GRBM_GUI_ACTIVE,"
                      "SQ_BUSY_CYCLES, each its own --kernel-trace pass over tools/prof_dit.py --forwards 1",
-           "box": a.box, "git_head": a.git,
+           "box": a.box, "git_head": a.git, "product_hash": _product_hash(),
            "note": "separate counter passes (not the bench's timed run); profiled passes run at a lower "
                    "clock than un-profiled ones (guide 'DVFS give-back' (2)); clock_GHz is withheld when "
                    "the GRBM quotient exceeds 2.4 GHz (short-dispatch bias)",
