@@ -25,7 +25,10 @@ dev = torch.device("cuda:0")
 SHAPES = {"swiglu": (6000, 12288, 2048, 3, 7, 256), "down": (6000, 2048, 6144, 2, 8, 192),
           "qkv": (6000, 4096, 2048, 0, 8, 192), "o": (6000, 2048, 2048, 2, 8, 192),
           "down256": (6000, 2048, 6144, 2, 7, 256), "swiglu_w4": (6000, 12288, 2048, 3, 11, 256),
-          "down_w4": (6000, 2048, 6144, 2, 11, 256), "qkv_w4": (6000, 4096, 2048, 0, 11, 256)}
+          "down_w4": (6000, 2048, 6144, 2, 11, 256), "qkv_w4": (6000, 4096, 2048, 0, 11, 256),
+          "o_half": (3000, 2048, 2048, 2, 13, 192)}
+# MFMA cycles per K-tile per SIMD when the loop is back-to-back (16 cycles per 16x16x32)
+IDEAL = {13: (96 // 16) * (64 // 16) * 2 * 16}
 if os.environ.get("SHAPES"):
     SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -45,7 +48,7 @@ for name, (M, N, K, epi, var, BM) in SHAPES.items():
     Ws = [W0] + [W0.clone() for _ in range(nrot - 1)]
     ldc = N // 2 if epi == 3 else N
     C = torch.randn(M, ldc, device=dev).bfloat16()
-    tiles = ((M + BM - 1) // BM) * (N // 256)
+    tiles = ((M + BM - 1) // BM) * (N // (128 if var == 13 else 256))
     for i in range(nrot + 2):
         assert lib.acehip_gemm_bf16_ex(A.data_ptr(), K, Ws[i % nrot].data_ptr(), K, C.data_ptr(), ldc, M, N, K,
                                        None, epi, var, stream) == 0
@@ -71,7 +74,7 @@ for name, (M, N, K, epi, var, BM) in SHAPES.items():
                      "xcc": s[6] & 0xffffffff})
     rows.sort(key=lambda r: r["start_us"])
     nk = K // 64
-    ideal = 2 * (BM // 2 // 16) * 4 * 2 * 16        # cycles per K-tile per SIMD at 16 cyc/MFMA, both waves
+    ideal = IDEAL.get(var, 2 * (BM // 2 // 16) * 4 * 2 * 16)   # cycles per K-tile per SIMD at 16 cyc/MFMA
     res = {"kernel_us_events": round(e0.elapsed_time(e1) * 1e3, 1),
            "span_us_real": round(max(r["end_us"] for r in rows), 1), "tiles": tiles, "nk": nk,
            "ideal_cyc_per_ktile": ideal, "rounds": []}
