@@ -786,8 +786,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 //            ∥ ds_reads of tile kt+1's k-step 0 → F0
 // so the MFMA pipe never waits for a fragment read, the DMA of a tile has one whole
 // K-tile (≈96 MFMAs) of lead, and two LDS buffers suffice.
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
+// NH > 0: NH extra helper waves issue every LDS-DMA piece (pieces q ≡ h mod NH), so the four
+// MFMA waves carry no DMA in their instruction stream (one wave per SIMD pays ≈ 60-185 cycles
+// per piece there); a helper waits for tile kt+1 before barrier kt and refills tile kt's buffer
+// after it, the same ordering as the MFMA waves' own refills
+template <int BM, int BN, int EPI, int NH = 0>
+__global__ __launch_bounds__(256 + 64 * NH, 1) void gemm_w4_kernel(GemmArgs a) {
     constexpr int TM = BM / 2, TN = BN / 2, SM = TM / 16, SN = TN / 16;
     constexpr int ROWS = BM + BN, STAGE = ROWS * 128;
     // ring depth: 3 tile buffers when they fit (a refill's DMA then has two K-tiles of lead,
@@ -810,6 +814,42 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     const int tm = first_m + (wg % per_group) % gsz;
     const int tn = (wg % per_group) / gsz;
     const int m0 = tm * BM, n0 = tn * BN;
+    const int nk = a.K / BK;
+
+    if constexpr (NH > 0) {
+        if (__builtin_amdgcn_readfirstlane(wave) >= 4) {
+            constexpr int PPH = 4 * PW / NH;                        // pieces per helper per K-tile
+            static_assert((4 * PW) % NH == 0 && (NS - 1) * PPH < 64, "helper pieces / vmcnt field");
+            const int h = wave - 4;
+            const bf16_t *hs[PPH];
+#pragma unroll
+            for (int i = 0; i < PPH; ++i) {
+                const int q = h + NH * i, r = q * 8 + (lane >> 3);
+                const int c = (lane & 7) ^ ((r >> 1) & 7);
+                if (r < BM) hs[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8;
+                else hs[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8;
+            }
+            auto fill = [&](int buf, int k0) {
+#pragma unroll
+                for (int i = 0; i < PPH; ++i) glds16(hs[i] + k0, lds + buf * STAGE + (h + NH * i) * 1024);
+            };
+            for (int t = 0; t < NS; ++t) fill(t, min(t, nk - 1) * BK);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PPH) : "memory");
+            __builtin_amdgcn_s_barrier();
+            for (int kt = 0; kt < nk; ++kt) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * PPH) : "memory");   // tile kt+1 landed
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                fill(kt % NS, min(kt + NS, nk - 1) * BK);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (EPI == EPI_HEADPOST) {   // the head-post epilogue's two block barriers
+                __syncthreads();
+                __syncthreads();
+            }
+            return;
+        }
+    }
 
     // staging: wave issues image rows [8q, 8q+8) for q = wave + 4i (swizzle on the source)
     const bf16_t *src[PW];
@@ -873,14 +913,15 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     // second copy of the MFMA code (a peeled tail) makes the register allocator move the
     // accumulators between copies with VALU instructions that the asm MFMAs — opaque
     // to the hazard recognizer — would read without the required wait states.
-    const int nk = a.K / BK;
     // prologue: tiles 0..NS−1 (clamped: duplicates past the last tile keep the count
     // uniform), tile 0 landed
+    if constexpr (NH == 0) {
 #pragma unroll
-    for (int t = 0; t < NS; ++t)
+        for (int t = 0; t < NS; ++t)
 #pragma unroll
-        for (int i = 0; i < PW; ++i) stage1(t, min(t, nk - 1) * BK, i);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
+            for (int i = 0; i < PW; ++i) stage1(t, min(t, nk - 1) * BK, i);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * PW) : "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     GSTAMP(1);
@@ -897,9 +938,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
         // refill of this tile's buffer (every wave is past its reads) with tile kt+NS
         const int kr = min(kt + NS, nk - 1) * BK;
         rd(lds + nxt * STAGE, 0, x0, w0);
-        mm(x1, w1, [&](int n) {
-            if (n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW) stage1(cur, kr, (n - FIRST) / EVERY);
-        });
+        if constexpr (NH == 0) {
+            mm(x1, w1, [&](int n) {
+                if (n >= FIRST && (n - FIRST) % EVERY == 0 && (n - FIRST) / EVERY < PW) stage1(cur, kr, (n - FIRST) / EVERY);
+            });
+        } else {
+            (void)kr;
+            mm(x1, w1, none);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the asm MFMAs are opaque to the hazard recognizer: let the last ones retire
@@ -926,18 +972,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a) {
     GSTAMP_REAL(5);
 }
 
-template <int BM, int BN = 256>
+template <int BM, int BN = 256, int NH = 0>
 int launch_w4(const GemmArgs &a, hipStream_t s) {
     if (a.N % BN) return fail(-1, "gemm: N not a multiple of the 4-wave tile");
     const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
+    constexpr int NT = 256 + 64 * NH;
     switch (a.epi) {
-        case EPI_STORE: gemm_w4_kernel<BM, BN, EPI_STORE><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_GATED_RES: gemm_w4_kernel<BM, BN, EPI_GATED_RES><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_RES: gemm_w4_kernel<BM, BN, EPI_RES><<<tiles, 256, 0, s>>>(a); break;
-        case EPI_SWIGLU: klaunch(gemm_w4_kernel<BM, BN, EPI_SWIGLU>, dim3(tiles), dim3(256), s, a); break;
+        case EPI_STORE: gemm_w4_kernel<BM, BN, EPI_STORE, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_w4_kernel<BM, BN, EPI_GATED_RES, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_RES: gemm_w4_kernel<BM, BN, EPI_RES, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_w4_kernel<BM, BN, EPI_SWIGLU, NH>, dim3(tiles), dim3(NT), s, a); break;
         case EPI_HEADPOST:
             if constexpr (BM == 192 && (BN == 256 || BN == 128)) {
-                gemm_w4_kernel<BM, BN, EPI_HEADPOST><<<tiles, 256, 0, s>>>(a);
+                gemm_w4_kernel<BM, BN, EPI_HEADPOST, NH><<<tiles, NT, 0, s>>>(a);
                 break;
             }
             return fail(-1, "gemm: the head-post epilogue needs the 192-row tile");
@@ -995,7 +1042,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 7: return knobs().gemm_ppsched == 2 ? launch_pp<256, 2>(a, s) : launch_pp<256, 1>(a, s);
         case 8: return knobs().gemm_ppsched == 2 ? launch_pp<192, 2>(a, s) : launch_pp<192, 0>(a, s);
         case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
-        case 13: return launch_w4<192, 128>(a, s);        // 4 waves, 96x64 wave tile (M≈3000 shapes: 1 round)
+        // 4 MFMA waves, 96x64 wave tiles, + 2 LDS-DMA helper waves (M≈3000 shapes: 1 round)
+        case 13: return launch_w4<192, 128, 2>(a, s);
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
         default: return fail(-1, "gemm: bad variant (0, 7, 8, 11, 13, 16)");
     }
@@ -1214,7 +1262,7 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
         // head_post kernel (the previous path), =0: the 192×256 grid regardless
         const int64_t t192 = (int64_t)((a.M + 191) / 192) * (a.N / 256);
         const bool small = t192 * 2 <= num_cus() && kn.gemm_hp128 != 0;
-        if (small && use_w4s(a.M, a.N) && kn.gemm_hp128 != 2) return launch_w4<192, 128>(a, s);
+        if (small && use_w4s(a.M, a.N) && kn.gemm_hp128 != 2) return gemm_variant(a, 13, s);
         if (small && a.ws && (size_t)a.M * a.N * 2 <= a.ws_bytes) {
             GemmArgs st = a;
             st.epi = EPI_STORE;
