@@ -1041,11 +1041,12 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         // (ACEHIP_GEMM_PPSCHED=1: the four-phase schedules, A/B)
         case 7: return knobs().gemm_ppsched == 2 ? launch_pp<256, 2>(a, s) : launch_pp<256, 1>(a, s);
         case 8: return knobs().gemm_ppsched == 2 ? launch_pp<192, 2>(a, s) : launch_pp<192, 0>(a, s);
+        case 9: return launch_pp<128, 2>(a, s);           // ping-pong 128x256, two phases per K-tile (96 KiB)
         case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
         // 4 MFMA waves, 96x64 wave tiles, + 2 LDS-DMA helper waves (M≈3000 shapes: 1 round)
         case 13: return launch_w4<192, 128, 2>(a, s);
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
-        default: return fail(-1, "gemm: bad variant (0, 7, 8, 11, 13, 16)");
+        default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 11, 13, 16)");
     }
 }
 
@@ -1217,7 +1218,9 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     tl.M = a.M - (int)M1;
     tl.A = a.A + M1 * a.lda;
     tl.C = a.C + M1 * a.ldc;
-    return gemm_variant(tl, 0, s);
+    // ACEHIP_GEMM_TAIL=1: the tail as one round of 128×256 two-phase ping-pong tiles
+    const bool pp128 = knobs().gemm_tail == 1 && a.N % 256 == 0 && ((tl.M + 127) / 128) * nN <= cus;
+    return gemm_variant(tl, pp128 ? 9 : 0, s);
 }
 
 int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {

@@ -8,7 +8,8 @@ namespace acehip {
 // A/B switches (knobs.hip): read from the ACEHIP_* environment once, on first use or by
 // acehip_reload_knobs(); gen counts reloads (part of the DiT graph key)
 struct Knobs {
-    int gemm_tailsplit = 1;   // ACEHIP_GEMM_TAILSPLIT: 0 off, 1 on, 2..9 the tail tile variant
+    int gemm_tailsplit = 1;   // ACEHIP_GEMM_TAILSPLIT: 0 off, 1 on
+    int gemm_tail = 1;        // ACEHIP_GEMM_TAIL: tail-split tile (1: 128×256 ping-pong, 0: 128×128)
     int gemm_w4s = 1;         // ACEHIP_GEMM_W4S: half-chip grids on the four-wave 192×128 tile
     int gemm_hp128 = 1;       // ACEHIP_GEMM_HP128: 0 / 2 alternative cross-Q head-post paths
     int gemm_ppsched = 2;     // ACEHIP_GEMM_PPSCHED: ping-pong schedule (2: two phases per K-tile, 1: four)

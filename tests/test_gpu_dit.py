@@ -45,7 +45,7 @@ def test_gemm(gpu_device, M, N, K):
 EPI_STORE, EPI_GATED_RES, EPI_RES, EPI_SWIGLU = 0, 1, 2, 3
 
 
-@pytest.mark.parametrize("variant", [0, 7, 8, 13, 16])
+@pytest.mark.parametrize("variant", [0, 7, 8, 9, 13, 16])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 64), (517, 256, 128), (200, 512, 192), (777, 768, 640)])
 def test_gemm_variants(gpu_device, variant, M, N, K):
     """Every production tile variant, odd K-tile counts (ring prologue/tail) and ragged M,
@@ -63,7 +63,7 @@ def test_gemm_pingpong_four_phase(gpu_device, monkeypatch, variant, M, N, K):
 
 def _gemm_variant_check(gpu_device, variant, M, N, K):
     ff = _lib()
-    if variant in (7, 8) and N % 256:
+    if variant in (7, 8, 9) and N % 256:
         pytest.skip("variant needs N % 256 == 0")
     g = torch.Generator(device="cpu").manual_seed(M * 3 + N + K + variant)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)

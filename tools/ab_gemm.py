@@ -19,7 +19,8 @@ from acehip import _ffi as ff  # noqa: E402
 dev = torch.device("cuda:0")
 # name: (M, N, K, epi, variant)  — epi 0 store, 3 SwiGLU; variants as the cost model picks them
 SHAPES = {"swiglu": (6000, 12288, 2048, 3, 7), "down": (6000, 2048, 6144, 2, 8), "qkv": (6000, 4096, 2048, 0, 8),
-          "o": (6000, 2048, 2048, 2, 8), "o_half": (3000, 2048, 2048, 2, 13), "crossq": (3000, 2048, 2048, 0, 13)}
+          "o": (6000, 2048, 2048, 2, 8), "o_half": (3000, 2048, 2048, 2, 13), "crossq": (3000, 2048, 2048, 0, 13),
+          "swiglu_prod": (6000, 12288, 2048, 3, -1)}   # -1: the production dispatch (tail split included)
 
 
 def load(path):
