@@ -49,11 +49,11 @@ __device__ __forceinline__ void stamp(int slot, int i, unsigned long long v) {
 }
 #define GSTAMP(i)                                                                                \
     do {                                                                                         \
-        if ((threadIdx.x & 255) == 0) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memtime()); \
+        if ((threadIdx.x & 255) == 0 && threadIdx.x < 512) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memtime()); \
     } while (0)
 #define GSTAMP_REAL(i)                                                                           \
     do {                                                                                         \
-        if ((threadIdx.x & 255) == 0) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memrealtime()); \
+        if ((threadIdx.x & 255) == 0 && threadIdx.x < 512) stamp(blockIdx.x * 2 + (threadIdx.x >> 8), i, __builtin_amdgcn_s_memrealtime()); \
     } while (0)
 #else
 #define GSTAMP(i) do {} while (0)
@@ -1043,8 +1043,9 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         case 8: return knobs().gemm_ppsched == 2 ? launch_pp<192, 2>(a, s) : launch_pp<192, 0>(a, s);
         case 9: return launch_pp<128, 2>(a, s);           // ping-pong 128x256, two phases per K-tile (96 KiB)
         case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
-        // 4 MFMA waves, 96x64 wave tiles, + 2 LDS-DMA helper waves (M≈3000 shapes: 1 round)
-        case 13: return launch_w4<192, 128, 2>(a, s);
+        // 4 MFMA waves, 96x64 wave tiles, + 2 LDS-DMA helper waves (M≈3000 shapes: 1 round;
+        // ACEHIP_GEMM_HELPERS=0: without, A/B)
+        case 13: return knobs().gemm_helpers ? launch_w4<192, 128, 2>(a, s) : launch_w4<192, 128>(a, s);
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
         default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 11, 13, 16)");
     }

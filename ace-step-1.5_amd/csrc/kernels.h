@@ -10,6 +10,7 @@ namespace acehip {
 struct Knobs {
     int gemm_tailsplit = 1;   // ACEHIP_GEMM_TAILSPLIT: 0 off, 1 on
     int gemm_tail = 1;        // ACEHIP_GEMM_TAIL: tail-split tile (1: 128×256 ping-pong, 0: 128×128)
+    int gemm_helpers = 1;     // ACEHIP_GEMM_HELPERS: LDS-DMA helper waves in the half-chip 4-wave tile
     int gemm_w4s = 1;         // ACEHIP_GEMM_W4S: half-chip grids on the four-wave 192×128 tile
     int gemm_hp128 = 1;       // ACEHIP_GEMM_HP128: 0 / 2 alternative cross-Q head-post paths
     int gemm_ppsched = 2;     // ACEHIP_GEMM_PPSCHED: ping-pong schedule (2: two phases per K-tile, 1: four)

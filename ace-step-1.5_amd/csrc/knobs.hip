@@ -20,6 +20,7 @@ Knobs read_env() {
     Knobs k;
     k.gemm_tailsplit = env_int("ACEHIP_GEMM_TAILSPLIT", 1);
     k.gemm_tail = env_int("ACEHIP_GEMM_TAIL", 1);
+    k.gemm_helpers = env_int("ACEHIP_GEMM_HELPERS", 1);
     k.gemm_w4s = env_int("ACEHIP_GEMM_W4S", 1);
     k.gemm_hp128 = env_int("ACEHIP_GEMM_HP128", 1);
     k.gemm_ppsched = env_int("ACEHIP_GEMM_PPSCHED", 2);

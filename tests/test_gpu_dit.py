@@ -61,6 +61,13 @@ def test_gemm_pingpong_four_phase(gpu_device, monkeypatch, variant, M, N, K):
     _gemm_variant_check(gpu_device, variant, M, N, K)
 
 
+@pytest.mark.parametrize("M,N,K", [(517, 256, 128), (777, 768, 640)])
+def test_gemm_four_wave_without_helpers(gpu_device, monkeypatch, M, N, K):
+    """The half-chip four-wave tile without its LDS-DMA helper waves (ACEHIP_GEMM_HELPERS=0, A/B arm)."""
+    set_knob(monkeypatch, "ACEHIP_GEMM_HELPERS", "0")
+    _gemm_variant_check(gpu_device, 13, M, N, K)
+
+
 def _gemm_variant_check(gpu_device, variant, M, N, K):
     ff = _lib()
     if variant in (7, 8, 9) and N % 256:
