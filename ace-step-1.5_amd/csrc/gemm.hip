@@ -446,33 +446,19 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
 // Ping-pong variant: BM×256 tile, 8 waves as 2 groups (wr = 0/1, A rows
 // [wr·BM/2, +BM/2)) × 4 (64 columns each).  The groups run one barrier apart,
 // so on every SIMD one wave issues MFMAs while the other issues LDS reads and
-// LDS-DMA (s_setprio(1) on the MFMA side).  Per K-tile, 4 phases of
-// [ds_read · (stage) · barrier · MFMA · barrier]:
-//   phase 0  read A-half0 + B0          stage A(kt+1) → other buffer
-//   phase 1  read B1
-//   phase 2  read A-half1
-//   phase 3  (B0, B1 still in regs)     stage B(kt+2) → this buffer's B slots,
-//                                        then vmcnt(#B glds): A(kt+1) landed
-// WAR: A(kt+1) overwrites tile kt−1's A, last read (group 1, phase 2) two
-// barriers earlier; B(kt+2) overwrites tile kt's B, last read in phase 1.
-// RAW: each wave's vmcnt precedes the barrier that opens the first read of
-// the tile (barrier 8kt+8 for group 0).  Two LDS tile buffers, ~1 tile of
-// DMA lead for A and ~1.25 for B.
-// SPL (SCHED 1 only): how the LDS-DMA pieces of a K-tile are spread over its phases —
-//   0  A(kt+1) all in phase 0, B(kt+2) all in phase 3
-//   1  A(kt+1) half in phase 0, half in phase 1; B(kt+2) all in phase 3
-//   2  A(kt+1) half in phase 0, half in phase 1; B(kt+2) first half in phase 3, second
-//      half in the next K-tile's phase 0 (as B(kt+1))
-//   3  as 2, but B(kt+1)'s second half in phase 1 (phase 0 carries only its 8 reads + 2);
-//      the 256-row default: interleaved 5-round medians (tools/bench_gemm.py ROUNDS=5, cold
-//      weights) SwiGLU 251.3 vs 257.3 µs, QKV 91.7 vs 95.0, down 128.6 vs 133.4 against 0
-//      (the ablation behind it: without the main-loop DMA the 256² tile ran 22 % faster,
-//      without the fragment reads 18 %, without both 37 %)
-// SCHED 0 takes SPL 1 only: A(kt+1) split between phases 0 and 1 (phase 3 has no reads)
-// SCHED 2: two phases per K-tile, each over both k-steps (half the barriers; 24 / 32 MFMAs
-// per interval at 192 / 256 rows): phase 0 reads all four B sub-tiles and A-half 0 and
-// stages A(kt+1), phase 1 reads A-half 1 and stages B(kt+2); reads retire before each barrier
-template <int BM, int EPI, int SPL = (BM == 256 ? 3 : 0), int SCHED = (BM == 256 ? 1 : 0)>
+// LDS-DMA (s_setprio(1) on the MFMA side).  Per K-tile, two phases of
+// [ds_read · (stage) · barrier · MFMA over both 32-deep k-steps · barrier]:
+//   phase 0  read the four B sub-tiles + A-half 0     stage A(kt+1) → other buffer
+//   phase 1  read A-half 1                             stage B(kt+2) → this buffer's B slots,
+//                                                       then vmcnt(#B glds): A(kt+1) landed
+// (24 / 32 MFMAs per interval at 192 / 256 rows; reads retire before each barrier).
+// WAR: A(kt+1) overwrites tile kt−1's A, last read by group 1's phase 1 of kt−1, retired
+// before this phase's opening barrier; B(kt+2) overwrites tile kt's B, last read by group 1's
+// phase 0, retired before the barrier that opens phase 1.  RAW: each wave's vmcnt precedes
+// the barrier that opens the first read of the tile.  Two LDS tile buffers.
+// Round 4 replaced a four-phase schedule (12 / 16 MFMAs per interval, 8
+// barriers per K-tile; stamps: the 192-row loop 62 % MFMA-busy, now 80 %): DESIGN.md.
+template <int BM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     constexpr int BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
     constexpr int ROWS = BM + BN, BUF = ROWS * 128;
@@ -524,16 +510,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) glds16(srcB[i] + k0, b + (wave + 8 * i) * 1024);
     };
-    auto stageAp = [&](int buf, int k0, int i0, int i1) {
-        char *b = lds + buf * BUF;
-#pragma unroll
-        for (int i = i0; i < i1; ++i) glds16(srcA[i] + k0, b + (wave + 8 * i) * 1024);
-    };
-    auto stageBp = [&](int buf, int k0, int i0, int i1) {
-        char *b = lds + buf * BUF + BM * 128;
-#pragma unroll
-        for (int i = i0; i < i1; ++i) glds16(srcB[i] + k0, b + (wave + 8 * i) * 1024);
-    };
     auto bar = [] {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -553,10 +529,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     // prologue: tile 0 complete, B(1) in flight
     stageB(0, 0);
     stageA(0, 0);
-    if (SPL >= 2 && nk > 1) {
-        stageBp(1, BK, 0, NB / 2);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB / 2) : "memory");
-    } else if (nk > 1) {
+    if (nk > 1) {
         stageB(1, BK);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
     } else {
@@ -566,9 +539,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     if (wr == 1) bar();   // group 1 runs one barrier behind
     GSTAMP(1);
 
-    static_assert(SCHED == 2 || SPL == 0 || SCHED == 1 || (SCHED == 0 && SPL == 1),
-                  "LDS-DMA spread: SCHED 1, or SPL 1 on SCHED 0");
-    if constexpr (SCHED == 2) {
+    {
     bf16x8 xa[SMH][2], bf[4][2];
     auto readA = [&](const char *b, int h) {
 #pragma unroll
@@ -615,140 +586,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
         mma(1);
         bar();
     }
-    } else if constexpr (SCHED == 1) {
-    // Balanced schedule: phase p multiplies A-half (p & 1) by all four B sub-tiles at
-    // k-step (p >> 1), so a loader wave issues 8, 4, 8, 4 ds_read_b128 per phase (the
-    // 12-read first phase of the schedule below, plus the A(kt+1) DMA, saturates the
-    // 256 B/clk LDS array against a 256-cycle MFMA phase) and holds 8 operand
-    // fragments instead of 16.  Reads complete (lgkmcnt(0)) BEFORE each barrier, so
-    // the WAR margins of the DMAs (A(kt+1) after tile kt−1's phase-3 reads, B(kt+2)
-    // after tile kt's phase-2 reads) are one barrier each.
-    bf16x8 xk[SMH], bk[4];
-    auto readA1 = [&](const char *b, int h, int ks) {
-#pragma unroll
-        for (int i = 0; i < SMH; ++i) xk[i] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
-    };
-    auto readB1 = [&](const char *b, int ks) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bk[j] = *(const bf16x8 *)(b + swz(brow + j * 16 + fr, ks * 4 + fc));
-    };
-    auto mma1 = [&](int h) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < SMH; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[h * SMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bk[j], xk[i], acc[h * SMH + i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    };
-    auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-    for (int kt = 0; kt < nk; ++kt) {
-        const char *b = lds + (kt & 1) * BUF;
-        readB1(b, 0);
-        readA1(b, 0, 0);
-        if (kt + 1 < nk) {
-            if constexpr (SPL == 0) stageA((kt + 1) & 1, (kt + 1) * BK);
-            else stageAp((kt + 1) & 1, (kt + 1) * BK, 0, NA / 2);
-            if constexpr (SPL == 2) stageBp((kt + 1) & 1, (kt + 1) * BK, NB / 2, NB);
-        }
-        lgkm0();
-        bar();
-        mma1(0);
-        bar();
-        readA1(b, 1, 0);
-        if (SPL != 0 && kt + 1 < nk) {
-            stageAp((kt + 1) & 1, (kt + 1) * BK, NA / 2, NA);
-            if constexpr (SPL == 3) stageBp((kt + 1) & 1, (kt + 1) * BK, NB / 2, NB);
-        }
-        lgkm0();
-        bar();
-        mma1(1);
-        bar();
-        readB1(b, 1);
-        readA1(b, 0, 1);
-        lgkm0();
-        bar();
-        mma1(0);
-        bar();
-        readA1(b, 1, 1);
-        if (SPL >= 2 && kt + 2 < nk) {
-            stageBp(kt & 1, (kt + 2) * BK, 0, NB / 2);
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB / 2) : "memory");
-        } else if (kt + 2 < nk) {
-            stageB(kt & 1, (kt + 2) * BK);
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NB) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        }
-        bar();
-        mma1(1);
-        bar();
-    }
-    } else {
-    bf16x8 xa[SMH][2], b0[2][2], b1[2][2];
-    auto readA = [&](const char *b, int h) {
-#pragma unroll
-        for (int i = 0; i < SMH; ++i)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-                xa[i][ks] = *(const bf16x8 *)(b + swz(arow + (h * SMH + i) * 16 + fr, ks * 4 + fc));
-    };
-    auto readB = [&](const char *b, int q, bf16x8 (&f)[2][2]) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-                f[j][ks] = *(const bf16x8 *)(b + swz(brow + (q * 2 + j) * 16 + fr, ks * 4 + fc));
-    };
-    auto mma = [&](int h, int q, const bf16x8 (&f)[2][2]) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int i = 0; i < SMH; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[h * SMH + i][q * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[j][ks], xa[i][ks], acc[h * SMH + i][q * 2 + j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    };
-    for (int kt = 0; kt < nk; ++kt) {
-        const char *b = lds + (kt & 1) * BUF;
-        // phase 0
-        readB(b, 0, b0);
-        readA(b, 0);
-        if (kt + 1 < nk) {
-            if constexpr (SPL == 1) stageAp((kt + 1) & 1, (kt + 1) * BK, 0, NA / 2);
-            else stageA((kt + 1) & 1, (kt + 1) * BK);
-        }
-        bar();
-        mma(0, 0, b0);
-        bar();
-        // phase 1
-        readB(b, 1, b1);
-        if (SPL == 1 && kt + 1 < nk) stageAp((kt + 1) & 1, (kt + 1) * BK, NA / 2, NA);
-        bar();
-        mma(0, 1, b1);
-        bar();
-        // phase 2
-        readA(b, 1);
-        bar();
-        mma(1, 1, b1);
-        bar();
-        // phase 3
-        if (kt + 2 < nk) {
-            stageB(kt & 1, (kt + 2) * BK);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        bar();
-        mma(1, 0, b0);
-        bar();
-    }
     }
     if (wr == 0) bar();   // balance the barrier count
     GSTAMP(2);
@@ -775,9 +612,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Four-wave variant: BM×256 tile, one wave per SIMD (2×2 waves, wave tile
-// (BM/2)×128: 48 or 64 accumulators of 16×16, in AGPRs), register double-buffered
-// fragments.  Per K-tile kt (two 32-deep k-steps), ONE barrier in the middle:
+// Four-wave variant: BM×BN tile, one wave per SIMD (2×2 waves, wave tile
+// (BM/2)×(BN/2): at the production 192×128, the half-chip M ≈ 3000 shapes, 24
+// accumulators of 16×16 in AGPRs), register double-buffered fragments.  Per K-tile kt (two 32-deep k-steps), ONE barrier in the middle:
 //   half A   MFMAs of k-step 0 (fragments F0)  ∥ ds_reads of k-step 1 → F1
 //   ──────   own LDS-DMA of tile kt+1 retired (vmcnt(0): nothing newer is in
 //            flight yet) + own reads retired, barrier: tile kt+1 is visible and
@@ -994,19 +831,18 @@ int launch_w4(const GemmArgs &a, hipStream_t s) {
     return 0;
 }
 
-template <int BM, int SCHED = (BM == 256 ? 1 : 0)>
+template <int BM>
 int launch_pp(const GemmArgs &a, hipStream_t s) {
     if (a.N % 256) return fail(-1, "gemm: N not a multiple of 256");
     const int tiles = ((a.M + BM - 1) / BM) * (a.N / 256);
-    constexpr int SP = SCHED == 2 ? 0 : (BM == 256 ? 3 : 0);
     switch (a.epi) {
-        case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_RES: gemm_pp_kernel<BM, EPI_RES, SP, SCHED><<<tiles, 512, 0, s>>>(a); break;
-        case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU, SP, SCHED>, dim3(tiles), dim3(512), s, a); break;
+        case EPI_STORE: gemm_pp_kernel<BM, EPI_STORE><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
         case EPI_HEADPOST:
             if constexpr (BM == 192 || BM == 128) {
-                gemm_pp_kernel<BM, EPI_HEADPOST, SP, SCHED><<<tiles, 512, 0, s>>>(a);
+                gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
                 break;
             }
             return fail(-1, "gemm: head-post epilogue needs the 192- or 128-row ping-pong tile");
@@ -1037,17 +873,15 @@ int launch(const GemmArgs &a, hipStream_t s) {
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
     switch (variant) {
         case 0: return launch<128, 128, 2, 2, 2>(a, s);   // 4 waves, 2-stage (2 blocks/CU): half-chip grids, tails
-        // ping-pong 256x256 (128 KiB) / 192x256 (112 KiB): two phases per K-tile
-        // (ACEHIP_GEMM_PPSCHED=1: the four-phase schedules, A/B)
-        case 7: return knobs().gemm_ppsched == 2 ? launch_pp<256, 2>(a, s) : launch_pp<256, 1>(a, s);
-        case 8: return knobs().gemm_ppsched == 2 ? launch_pp<192, 2>(a, s) : launch_pp<192, 0>(a, s);
-        case 9: return launch_pp<128, 2>(a, s);           // ping-pong 128x256, two phases per K-tile (96 KiB)
-        case 11: return launch_w4<256>(a, s);             // 4 waves (1/SIMD), 128x128 wave tiles, acc in AGPRs
+        // two-phase ping-pong tiles: 256x256 (128 KiB), 192x256 (112 KiB), 128x256 (96 KiB)
+        case 7: return launch_pp<256>(a, s);
+        case 8: return launch_pp<192>(a, s);
+        case 9: return launch_pp<128>(a, s);
         // 4 MFMA waves, 96x64 wave tiles, + 2 LDS-DMA helper waves (M≈3000 shapes: 1 round;
         // ACEHIP_GEMM_HELPERS=0: without, A/B)
         case 13: return knobs().gemm_helpers ? launch_w4<192, 128, 2>(a, s) : launch_w4<192, 128>(a, s);
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
-        default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 11, 13, 16)");
+        default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 13, 16)");
     }
 }
 

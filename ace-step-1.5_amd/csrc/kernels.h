@@ -13,7 +13,6 @@ struct Knobs {
     int gemm_helpers = 1;     // ACEHIP_GEMM_HELPERS: LDS-DMA helper waves in the half-chip 4-wave tile
     int gemm_w4s = 1;         // ACEHIP_GEMM_W4S: half-chip grids on the four-wave 192×128 tile
     int gemm_hp128 = 1;       // ACEHIP_GEMM_HP128: 0 / 2 alternative cross-Q head-post paths
-    int gemm_ppsched = 2;     // ACEHIP_GEMM_PPSCHED: ping-pong schedule (2: two phases per K-tile, 1: four)
     int splitk_fuse = 1;      // ACEHIP_SPLITK_FUSE: split-K epilogues folded into their consumers
     int splitk_bn = 0;        // ACEHIP_SPLITK_BN: 0 auto, 64 / 128 forced
     int smallm_wholek = 1;    // ACEHIP_SMALLM_WHOLEK: M ≤ 128 SwiGLU on whole-K 128×64 tiles

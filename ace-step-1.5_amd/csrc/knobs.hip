@@ -23,7 +23,6 @@ Knobs read_env() {
     k.gemm_helpers = env_int("ACEHIP_GEMM_HELPERS", 1);
     k.gemm_w4s = env_int("ACEHIP_GEMM_W4S", 1);
     k.gemm_hp128 = env_int("ACEHIP_GEMM_HP128", 1);
-    k.gemm_ppsched = env_int("ACEHIP_GEMM_PPSCHED", 2);
     k.splitk_fuse = env_int("ACEHIP_SPLITK_FUSE", 1);
     k.splitk_bn = env_int("ACEHIP_SPLITK_BN", 0);
     k.smallm_wholek = env_int("ACEHIP_SMALLM_WHOLEK", 1);

@@ -53,14 +53,6 @@ def test_gemm_variants(gpu_device, variant, M, N, K):
     _gemm_variant_check(gpu_device, variant, M, N, K)
 
 
-@pytest.mark.parametrize("variant", [7, 8])
-@pytest.mark.parametrize("M,N,K", [(517, 256, 128), (777, 768, 640)])
-def test_gemm_pingpong_four_phase(gpu_device, monkeypatch, variant, M, N, K):
-    """The four-phase ping-pong schedules (ACEHIP_GEMM_PPSCHED=1, the A/B arm)."""
-    set_knob(monkeypatch, "ACEHIP_GEMM_PPSCHED", "1")
-    _gemm_variant_check(gpu_device, variant, M, N, K)
-
-
 @pytest.mark.parametrize("M,N,K", [(517, 256, 128), (777, 768, 640)])
 def test_gemm_four_wave_without_helpers(gpu_device, monkeypatch, M, N, K):
     """The half-chip four-wave tile without its LDS-DMA helper waves (ACEHIP_GEMM_HELPERS=0, A/B arm)."""

@@ -24,8 +24,7 @@ dev = torch.device("cuda:0")
 # name: (M, N, K, epi, variant, BM)
 SHAPES = {"swiglu": (6000, 12288, 2048, 3, 7, 256), "down": (6000, 2048, 6144, 2, 8, 192),
           "qkv": (6000, 4096, 2048, 0, 8, 192), "o": (6000, 2048, 2048, 2, 8, 192),
-          "down256": (6000, 2048, 6144, 2, 7, 256), "swiglu_w4": (6000, 12288, 2048, 3, 11, 256),
-          "down_w4": (6000, 2048, 6144, 2, 11, 256), "qkv_w4": (6000, 4096, 2048, 0, 11, 256),
+          "down256": (6000, 2048, 6144, 2, 7, 256),
           "o_half": (3000, 2048, 2048, 2, 13, 192)}
 # MFMA cycles per K-tile per SIMD when the loop is back-to-back (16 cycles per 16x16x32)
 IDEAL = {13: (96 // 16) * (64 // 16) * 2 * 16}
