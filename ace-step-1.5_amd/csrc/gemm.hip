@@ -203,8 +203,10 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
     }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
-__global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
+// NH > 0: NH helper waves issue every LDS-DMA piece (q ≡ h mod NH) with the same counted
+// waits and barriers, so the NW MFMA waves (one per SIMD at NW = 4) carry no DMA in their stream
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int NH = 0>
+__global__ __launch_bounds__(WM *WN * 64 + 64 * NH, 1) void gemm_kernel(GemmArgs a) {
     constexpr int NW = WM * WN;
     constexpr int TM = BM / WM, TN = BN / WN;          // wave tile
     constexpr int SM = TM / 16, SN = TN / 16;          // 16×16 sub-tiles per wave
@@ -229,6 +231,37 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
     const int tm = first_m + (wg % per_group) % gsz;
     const int tn = (wg % per_group) / gsz;
     const int m0 = tm * BM, n0 = tn * BN;
+    const int nk = EPI == EPI_PARTIAL ? min(a.kper, a.K / BK - ktile0) : a.K / BK;
+
+    if constexpr (NH > 0) {
+        if (__builtin_amdgcn_readfirstlane(wave) >= NW) {
+            constexpr int PPH = NINS / NH;
+            static_assert(NINS % NH == 0 && (STAGES - 1) * PPH < 64, "helper pieces / vmcnt field");
+            const int h = wave - NW;
+            const bf16_t *hs[PPH];
+#pragma unroll
+            for (int i = 0; i < PPH; ++i) {
+                const int q = h + NH * i, r = q * 8 + (lane >> 3);
+                const int c = (lane & 7) ^ ((r >> 1) & 7);
+                if (r < BM) hs[i] = a.A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 8 + ktile0 * BK;
+                else hs[i] = a.W + (int64_t)(n0 + r - BM) * a.ldw + c * 8 + ktile0 * BK;
+            }
+            auto hst = [&](int buf, int k0) {
+#pragma unroll
+                for (int i = 0; i < PPH; ++i) glds16(hs[i] + k0, lds + buf * STAGE + (h + NH * i) * 1024);
+            };
+#pragma unroll
+            for (int s2 = 0; s2 < STAGES - 1; ++s2)
+                if (s2 < nk) hst(s2, s2 * BK);
+            for (int kt = 0; kt < nk; ++kt) {
+                if (kt + STAGES - 2 < nk) ring_barrier<(STAGES - 2) * PPH>();
+                else ring_barrier<0>();
+                if (kt + STAGES - 1 < nk) hst((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+    }
 
     // staging sources: wave issues image rows [8q, 8q+8) for q = wave + NW·i
     const bf16_t *src[PER_WAVE];
@@ -252,17 +285,22 @@ __global__ __launch_bounds__(WM *WN * 64, 1) void gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < SN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = EPI == EPI_PARTIAL ? min(a.kper, a.K / BK - ktile0) : a.K / BK;
+    if constexpr (NH == 0) {
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) stage(s, s * BK);
+        for (int s = 0; s < STAGES - 1; ++s)
+            if (s < nk) stage(s, s * BK);
+    }
     const int fr = lane & 15, fc = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt landed (its own wave's DMAs), leaving STAGES-2 newer tiles in flight
         // every wave's DMA for tile kt landed; tile kt-1 fully read (WAR for the refill below)
-        if (kt + STAGES - 2 < nk) ring_barrier<(STAGES - 2) * PER_WAVE>();
-        else ring_barrier<0>();
-        if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+        if constexpr (NH > 0) {
+            ring_barrier<0>();   // own reads retired (no DMA of its own); the helpers waited
+        } else {
+            if (kt + STAGES - 2 < nk) ring_barrier<(STAGES - 2) * PER_WAVE>();
+            else ring_barrier<0>();
+            if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+        }
         const char *b = lds + (kt % STAGES) * STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -852,16 +890,16 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
     return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int NH = 0>
 int launch(const GemmArgs &a, hipStream_t s) {
     if (a.N % BN) return fail(-1, "gemm: N not a multiple of the tile");
     const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-    constexpr int NT = WM * WN * 64;
+    constexpr int NT = WM * WN * 64 + 64 * NH;
     switch (a.epi) {
-        case EPI_STORE: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_STORE><<<tiles, NT, 0, s>>>(a); break;
-        case EPI_GATED_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_GATED_RES><<<tiles, NT, 0, s>>>(a); break;
-        case EPI_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_RES><<<tiles, NT, 0, s>>>(a); break;
-        case EPI_SWIGLU: klaunch(gemm_kernel<BM, BN, WM, WN, STAGES, EPI_SWIGLU>, dim3(tiles), dim3(NT), s, a); break;
+        case EPI_STORE: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_STORE, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_GATED_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_GATED_RES, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_RES: gemm_kernel<BM, BN, WM, WN, STAGES, EPI_RES, NH><<<tiles, NT, 0, s>>>(a); break;
+        case EPI_SWIGLU: klaunch(gemm_kernel<BM, BN, WM, WN, STAGES, EPI_SWIGLU, NH>, dim3(tiles), dim3(NT), s, a); break;
         default: return fail(-1, "gemm: bad epilogue for this variant");
     }
     HIP_TRY(hipGetLastError());
@@ -881,7 +919,8 @@ int gemm_variant(const GemmArgs &a, int variant, hipStream_t s) {
         // ACEHIP_GEMM_HELPERS=0: without, A/B)
         case 13: return knobs().gemm_helpers ? launch_w4<192, 128, 2>(a, s) : launch_w4<192, 128>(a, s);
         case 16: return launch<128, 64, 4, 1, 4>(a, s);   // 4 waves × 32 rows × 64 columns, 4-stage: M ≤ 128 SwiGLU
-        default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 13, 16)");
+        case 17: return launch<128, 64, 4, 1, 4, 2>(a, s);  // 16 + two LDS-DMA helper waves (M ≤ 128 SwiGLU)
+        default: return fail(-1, "gemm: bad variant (0, 7, 8, 9, 13, 16, 17)");
     }
 }
 
@@ -957,14 +996,15 @@ int gemm_pick_variant(int64_t M, int N) {
 static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipStream_t s);
 
 // split-K tile width: 64-column tiles double the grid at a given split count (half the splits
-// and partial bytes for ~1 block per CU).  Measured at M = 125, cold weights, one process
-// (tools/bench_small_m.py, profiles/r03_small_m.log): down (N 2048, K 6144) 19.9 → 17.9 µs,
-// QKV (N 4096, K 2048) 18.8 → 17.2, but O (N 2048, K 2048: 4 K-tiles per split) 18.7 → 25.3 —
-// so 64 where N or K ≥ 4096.  ACEHIP_SPLITK_BN = 128 | 64 forces one (A/B)
-static int splitk_bn(const GemmArgs &a) {
+// and partial bytes for ~1 block per CU).  Round 3 kept 128 where N and K < 4096 (O at M = 125
+// measured 18.7 → 25.3 µs on 64); round 4 measured every shape faster on 64 (O 16.0 → 14.7, QKV
+// 15.4 → 14.8, `profiles/r04h2_small_m.log`) and the songs too (turbo 10 s DiT 25.6 → 24.6 ms,
+// base 10 s 96.9 → 93.9, `profiles/r04h3_ab_turbo.log`): 64 everywhere.  ACEHIP_SPLITK_BN =
+// 128 | 64 forces one (A/B)
+static int splitk_bn(const GemmArgs &) {
     const int f = knobs().splitk_bn;
     if (f) return f == 64 ? 64 : 128;
-    return (a.N >= 4096 || a.K >= 4096) ? 64 : 128;
+    return 64;
 }
 static void fill_defer(const GemmArgs &a, int splits, RowAdd *defer);
 static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s, RowAdd *defer = nullptr) {
@@ -974,6 +1014,7 @@ static int gemm_splitk(const GemmArgs &a, int splits, hipStream_t s, RowAdd *def
     splits = (nk + p.kper - 1) / p.kper;
     const int bn = splitk_bn(a);
     const int tiles = ((a.M + 127) / 128) * (a.N / bn);
+    // (helper waves measured no gain here: 2 MFMA waves / SIMD already cover the DMA issue)
     if (bn == 64) gemm_kernel<128, 64, 4, 1, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     else if (a.N <= 4096) gemm_kernel<128, 128, 2, 2, 3, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
     else gemm_kernel<128, 128, 2, 2, 2, EPI_PARTIAL><<<dim3(tiles, splits), 256, 0, s>>>(p);
@@ -1081,7 +1122,7 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
     // SwiGLU of one 128-row chunk (turbo / short songs, M ≤ 128): whole-K 128×64 tiles with the
     // SwiGLU epilogue fused (variant 16: no fp32 partials, no second launch) — M = 125, cold
     // weights: 26.1 → 19.0 µs (tools/bench_small_m.py).  ACEHIP_SMALLM_WHOLEK=0: split-K (A/B)
-    if (a.epi == EPI_SWIGLU && a.M <= 128 && a.N % 64 == 0 && kn.smallm_wholek) return gemm_variant(a, 16, s);
+    if (a.epi == EPI_SWIGLU && a.M <= 128 && a.N % 64 == 0 && kn.smallm_wholek) return gemm_variant(a, kn.smallm_wholek == 2 ? 17 : 16, s);
     if (a.ws && a.N % 128 == 0 && a.K % BK == 0 && (a.N % 256 == 0 || a.epi != EPI_HEADPOST)) {
         const int cus = num_cus();
         const int64_t tiles = ((a.M + 127) / 128) * (a.N / 128);

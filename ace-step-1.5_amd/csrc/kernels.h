@@ -15,7 +15,7 @@ struct Knobs {
     int gemm_hp128 = 1;       // ACEHIP_GEMM_HP128: 0 / 2 alternative cross-Q head-post paths
     int splitk_fuse = 1;      // ACEHIP_SPLITK_FUSE: split-K epilogues folded into their consumers
     int splitk_bn = 0;        // ACEHIP_SPLITK_BN: 0 auto, 64 / 128 forced
-    int smallm_wholek = 1;    // ACEHIP_SMALLM_WHOLEK: M ≤ 128 SwiGLU on whole-K 128×64 tiles
+    int smallm_wholek = 2;    // ACEHIP_SMALLM_WHOLEK: M ≤ 128 SwiGLU on whole-K 128×64 tiles (2: + DMA helper waves, 1: without, 0: split-K)
     int attn_pw = 2;          // ACEHIP_ATTN_PW: layer kinds on attn_pw_kernel (1 full, 2 band, 4 cross)
     int attn_persist = 1;     // ACEHIP_ATTN_PERSIST: persistent band units
     int attn_pw_split = 24;   // ACEHIP_ATTN_PW_SPLIT: shortest KV loop whose tail units are split

@@ -25,7 +25,7 @@ Knobs read_env() {
     k.gemm_hp128 = env_int("ACEHIP_GEMM_HP128", 1);
     k.splitk_fuse = env_int("ACEHIP_SPLITK_FUSE", 1);
     k.splitk_bn = env_int("ACEHIP_SPLITK_BN", 0);
-    k.smallm_wholek = env_int("ACEHIP_SMALLM_WHOLEK", 1);
+    k.smallm_wholek = env_int("ACEHIP_SMALLM_WHOLEK", 2);
     k.attn_pw = env_int("ACEHIP_ATTN_PW", 2);
     k.attn_persist = env_int("ACEHIP_ATTN_PERSIST", 1);
     k.attn_pw_split = env_int("ACEHIP_ATTN_PW_SPLIT", 24);

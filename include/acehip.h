@@ -346,7 +346,8 @@ int acehip_gemm_bf16(const void *A, int lda, const void *W, int ldw, void *C, in
  * 3 SwiGLU: W rows packed [32 gate; 32 up] per 64-row panel, C is [M][N/2])
  * and tile variant (0: 128x128 2-stage, 7: 256x256 ping-pong, 8: 192x256
  * ping-pong, 9: 128x256 ping-pong (7-9: N % 256 == 0), 13: four-wave 192x128
- * + DMA helper waves (N % 128 == 0), 16: 128x64 4-stage;
+ * + DMA helper waves (N % 128 == 0), 16: 128x64 4-stage, 17: 16 + two DMA
+ * helper waves (N % 64 == 0);
  * -1: the production choice, including the tail split and split-K for grids that
  * cannot fill half the chip) — tuning and tests. */
 int acehip_gemm_bf16_ex(const void *A, int lda, const void *W, int ldw, void *C, int ldc,

@@ -45,7 +45,7 @@ def test_gemm(gpu_device, M, N, K):
 EPI_STORE, EPI_GATED_RES, EPI_RES, EPI_SWIGLU = 0, 1, 2, 3
 
 
-@pytest.mark.parametrize("variant", [0, 7, 8, 9, 13, 16])
+@pytest.mark.parametrize("variant", [0, 7, 8, 9, 13, 16, 17])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 64), (517, 256, 128), (200, 512, 192), (777, 768, 640)])
 def test_gemm_variants(gpu_device, variant, M, N, K):
     """Every production tile variant, odd K-tile counts (ring prologue/tail) and ragged M,
@@ -634,8 +634,9 @@ def test_forward_graph_replay_matches_eager(gpu_device):
                                        (250, 4096, 2048, EPI_STORE), (125, 2048, 2048, EPI_RES)])
 def test_gemm_small_m_paths(gpu_device, monkeypatch, M, N, K, epi):
     """Turbo / short-song GEMMs (M ≤ 256): SwiGLU of one 128-row chunk on whole-K 128×64 tiles
-    with the epilogue fused (ACEHIP_SMALLM_WHOLEK), and the split-K path on 64- or 128-column
-    tiles (ACEHIP_SPLITK_BN, default 64 where N or K ≥ 4096): every variant vs fp32 torch."""
+    with the epilogue fused (ACEHIP_SMALLM_WHOLEK: 2 default, + DMA helper waves; 1 without),
+    and the split-K path on 64- or 128-column tiles (ACEHIP_SPLITK_BN, default 64): every
+    variant vs fp32 torch."""
     ff = _lib()
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
     A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -647,7 +648,8 @@ def test_gemm_small_m_paths(gpu_device, monkeypatch, M, N, K, epi):
         y = ref.bfloat16().float().view(M, N // 64, 2, 32)
         gate, up = y[:, :, 0, :].reshape(M, ncol), y[:, :, 1, :].reshape(M, ncol)
         want, tol = torch.nn.functional.silu(gate).bfloat16().float() * up, 1e-2
-        knobs = [{"ACEHIP_SMALLM_WHOLEK": "1"}, {"ACEHIP_SMALLM_WHOLEK": "0"}]
+        knobs = [{}, {"ACEHIP_SMALLM_WHOLEK": "1"}, {"ACEHIP_SMALLM_WHOLEK": "0"},
+                 {"ACEHIP_SMALLM_WHOLEK": "0", "ACEHIP_SPLITK_BN": "128"}]
     else:
         want, tol = ref + (C0.float() if epi == EPI_RES else 0), (1e-2 if epi == EPI_RES else 5e-3)
         knobs = [{}, {"ACEHIP_SPLITK_BN": "64"}, {"ACEHIP_SPLITK_BN": "128"}]

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Small-M GEMM A/B at the turbo / short-song shapes (M = Bc·S = 125 at 10 s turbo): the
-production dispatch (128×128 split-K + its epilogue launch) against 64-column split-K tiles
-(ACEHIP_SPLITK_BN=64) and whole-K narrow tiles with the epilogue fused (variant 16),
+production dispatch (64-column split-K + its epilogue launch; SwiGLU on whole-K 128×64 tiles
+with helper waves, variant 17) against 128-column split-K tiles (ACEHIP_SPLITK_BN=128) and
+the whole-K tiles without helpers (variant 16),
 cold weights (rotated copies > 600 MB), interleaved rounds in one process, medians."""
 import json, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,7 +14,7 @@ dev = torch.device("cuda:0")
 M = int(os.environ.get("M", "125"))
 # name: (N, K, epi)  epi 0 store, 2 residual (C += A·Wᵀ), 3 SwiGLU (C[M][N/2])
 shapes = {"swiglu": (12288, 2048, 3), "down": (2048, 6144, 2), "qkv": (4096, 2048, 0), "o": (2048, 2048, 2)}
-cases = {"prod": (-1, {}), "bn64": (-1, {"ACEHIP_SPLITK_BN": "64"}), "v16": (16, {})}
+cases = {"prod": (-1, {}), "bn128": (-1, {"ACEHIP_SPLITK_BN": "128"}), "v16": (16, {}), "v17": (17, {})}
 if os.environ.get("SHAPES"):
     shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
 if os.environ.get("CASES"):        # extra env cases: "name:K=V+K=V;name2:K=V"
