@@ -1097,12 +1097,27 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const bf16_t *__restrict_
     // LDS-issue-bound (2.36 ms per 240 s decode, 1.25 TB/s of its 2.95 GB input)
     char *xs = smem;                                   // [P][Cin] bf16, swizzled chunks
     const int64_t t0 = (int64_t)blockIdx.x * 256;
-    for (int c = threadIdx.x; c < P * chunks; c += 256) {
+    // every 16-B load of the window in flight before the first LDS store: a load → wait →
+    // store loop paid one full memory latency per chunk (17 per block at Cin = 128)
+    constexpr int NCH = P * (CIN / 8), ITER = (NCH + 255) / 256;
+    uint4 v[ITER];
+    // (straight-line: clamped addresses, out-of-range rows zeroed at the store — a guarded load
+    // per chunk made hipcc wait vmcnt(0) at every branch merge)
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+        const int c = min(threadIdx.x + 256 * i, NCH - 1);
+        const int64_t pos = t0 - 3 + c / chunks;
+        v[i] = *(const uint4 *)(in + min(max(pos, (int64_t)0), L - 1) * Cin + (c % chunks) * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);      // every load issued before the first store
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+        const int c = threadIdx.x + 256 * i;
         const int p = c / chunks, ch = c % chunks;
         const int64_t pos = t0 - 3 + p;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (pos >= 0 && pos < L) v = *(const uint4 *)(in + pos * Cin + ch * 8);
-        *(uint4 *)(xs + (size_t)p * Cin * 2 + ((ch ^ (p & cm)) << 4)) = v;
+        const bool ok = pos >= 0 && pos < L;
+        const uint4 x = make_uint4(ok ? v[i].x : 0u, ok ? v[i].y : 0u, ok ? v[i].z : 0u, ok ? v[i].w : 0u);
+        if (i + 1 < ITER || c < NCH) *(uint4 *)(xs + (size_t)p * Cin * 2 + ((ch ^ (p & cm)) << 4)) = x;
     }
     __syncthreads();
     const int64_t t = t0 + threadIdx.x;
