@@ -1069,6 +1069,333 @@ __global__ __launch_bounds__(256, 2) void ru7_kernel(ResUnitArgs u, int64_t ntil
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same residual unit on 256-row tiles, one block per CU (ru8_kernel).  ru7_kernel streams
+// the whole 256 KiB W1 | W2 stream through LDS once per 128 rows, one K-tile ahead, and its MFMA
+// waves issue those LDS-DMA pieces themselves: per tile the W refill alone measured 2.7 of the
+// ≈ 6 ms of a 11.52 M-row unit (r02), MFMA-busy 33 %.  Here:
+//  * four MFMA waves own 64 rows × 128 channels each (4 row fragments: 128 accumulators), so the
+//    W stream is paid once per 256 rows, and W(kt) is consumed by 4 × 64 MFMAs per wave;
+//  * two helper waves issue every LDS-DMA piece (window chunks and W K-tiles) — the MFMA waves
+//    carry none in their stream (the GEMM's half-chip tile measured the same lever);
+//  * W runs through a 3-slot ring two K-tiles ahead (W(kt+2) issued behind barrier kt into the
+//    slot of K-tile kt−1): a piece has two K-tile intervals (≈ 1 µs) to land.
+// Helper step kt (behind barrier kt) issues its window pieces first, then W: the chunk-1 window
+// of THIS tile (pieces 14-38, steps 0-3 — not for the block's first tile, whose windows the
+// prologue stages whole), the chunk-0 window of the NEXT tile (steps 7-12: buffer 0 was last
+// read at K-tile 6) and the first part of its chunk 1 (steps 14-15: buffer 1 last read at 13),
+// then W(kt+2) (steps 14-15: W(0), W(1) of the next tile).  Before barrier kt a helper waits
+// until at most the pieces of its step kt−1 are in flight: W(kt) and every window piece issued
+// before it have landed (vmcnt retires in order), and every chunk a K-tile reads was issued
+// before the W that K-tile's barrier waits for.
+// LDS: 2 560 (parameters) + 2 × 39 680 (windows: 310 rows × 64 channels) + 3 × 16 KiB = 128 KiB.
+template <int I0, int I1, typename F>
+__device__ __forceinline__ void sfor(F &&f) {     // compile-time unrolled loop (f gets an integral_constant)
+    if constexpr (I0 < I1) {
+        f(std::integral_constant<int, I0>{});
+        sfor<I0 + 1, I1>(f);
+    }
+}
+namespace ru8 {
+constexpr int BM = 256, WROWS = 310, WINB = WROWS * 128, WT = 128 * 128, PAR = 2560, NSLOT = 3;
+constexpr int LDS = PAR + 2 * WINB + NSLOT * WT;
+constexpr int NPW = (WROWS + 7) / 8;   // 39 window pieces (8 rows) per chunk; the last is 6 rows
+static_assert(LDS <= 160 * 1024, "LDS");
+static_assert(BM + 54 <= WROWS, "halo of dilation 9");
+// window piece ranges per helper step: chunk 0 of the next tile over steps 7-12; chunk 1 of the
+// next tile over steps 14-15 (pieces 0-13) and of the current one over steps 0-3 (14-38)
+__host__ __device__ constexpr int c0_lo(int s) { return s == 0 ? 0 : s == 1 ? 7 : s == 2 ? 14 : s == 3 ? 20 : s == 4 ? 26 : 33; }
+__host__ __device__ constexpr int c0_hi(int s) { return s == 5 ? NPW : c0_lo(s + 1); }
+__host__ __device__ constexpr int c1a_lo(int s) { return s == 0 ? 0 : 7; }
+__host__ __device__ constexpr int c1a_hi(int s) { return s == 0 ? 7 : 14; }
+__host__ __device__ constexpr int c1b_lo(int s) { return s == 0 ? 14 : s == 1 ? 20 : s == 2 ? 26 : 33; }
+__host__ __device__ constexpr int c1b_hi(int s) { return s == 3 ? NPW : c1b_lo(s + 1); }
+// pieces q in [a, b) with q % 2 == h (helper h's share)
+__host__ __device__ constexpr int share(int a, int b, int h) { return (b - h + 1) / 2 - (a - h + 1) / 2; }
+// DMA instructions helper h issues in step s (window pieces + 8 W pieces), for a tile that is
+// (not) the block's first and has (no) successor
+__host__ __device__ constexpr int step_count(int s, int h, bool first, bool more) {
+    int n = 0;
+    if (s <= 3 && !first) n += share(c1b_lo(s), c1b_hi(s), h);
+    if (s >= 7 && s <= 12 && more) n += share(c0_lo(s - 7), c0_hi(s - 7), h);
+    if (s >= 14 && more) n += share(c1a_lo(s - 14), c1a_hi(s - 14), h);
+    if (s <= 13 || more) n += 8;
+    return n;
+}
+}  // namespace ru8
+
+// vmcnt(N) with N a template constant (N ≤ 63)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// helper h's window pieces q ∈ [P0, P1), q ≡ h (mod 2), of 64-channel chunk cc for the tile at m0
+template <int P0, int P1>
+__device__ __forceinline__ void ru8_win(const ConvArgs &a, uint32_t buf, int64_t m0, uint32_t voff, int lane, int h) {
+    const char *base = (const char *)(a.in + (m0 - 3 * a.dil) * 128);
+    asm volatile("" : "+s"(base));
+#pragma unroll
+    for (int q = P0; q < P1; ++q) {
+        if ((q & 1) != h) continue;
+        if (q * 8 + 8 <= ru8::WROWS || (lane >> 3) < ru8::WROWS - q * 8)
+            ru_dma(base + q * 8 * 256, buf + q * 1024, voff);
+    }
+}
+// helper h's 8 pieces (q ≡ h mod 2) of W K-tile kt into the ring slot at LDS address `slot`
+// (the source base passes through an opaque asm per call: otherwise hipcc hoists the 128
+// loop-invariant (K-tile, piece) addresses of the unrolled step sequence into SGPRs and spills them)
+__device__ __forceinline__ void ru8_w(const ResUnitArgs &u, uint32_t slot, int kt, int h, uint32_t voff1,
+                                      uint32_t voff2) {
+    const char *w1 = (const char *)u.c1.W, *w2 = (const char *)u.W2p;
+    asm volatile("" : "+s"(w1), "+s"(w2));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = h + 2 * i;
+        if (kt < 14) {
+            const int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
+            ru_dma(w1 + q * 8 * 1792 + tap * 256 + cc * 128, slot + q * 1024, voff1);
+        } else {
+            ru_dma(w2 + q * 8 * 256 + (kt - 14) * 128, slot + q * 1024, voff2);
+        }
+    }
+}
+
+template <bool RAW>
+__global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
+    constexpr int RBM = ru8::BM, WINB = ru8::WINB, WT = ru8::WT;
+    __shared__ __attribute__((aligned(16))) char lds[ru8::LDS];
+    const ConvArgs &a = u.c1;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
+    char *par = lds, *win = lds + ru8::PAR, *wr = win + 2 * WINB;
+    const uint32_t win3 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds + ru8::PAR;
+    const uint32_t wr3 = win3 + 2 * WINB;
+    float *psa2 = (float *)par, *psib2 = psa2 + 128, *psan = psa2 + 256, *psibn = psa2 + 384;
+    bf16_t *pb1 = (bf16_t *)(par + 2048), *pb2 = (bf16_t *)(par + 2304);
+
+    if (wave >= 4) {
+        // ---- helper waves: every LDS-DMA of the block ----
+        const int h = wave - 4;
+        const int l3 = lane >> 3, lc = ((lane & 7) ^ l3) * 16;
+        const uint32_t vw0 = l3 * 256 + lc, vw1 = vw0 + 128;          // window chunk 0 / 1
+        const uint32_t vk1 = l3 * 1792 + lc, vk2 = l3 * 256 + lc;       // W1 / W2 rows
+        // prologue: chunk 0, W(0), chunk 1, W(1); barrier 0 needs chunk 0 and W(0)
+        ru8_win<0, ru8::NPW>(a, win3, t0 * RBM, vw0, lane, h);
+        ru8_w(u, wr3, 0, h, vk1, vk2);
+        ru8_win<0, ru8::NPW>(a, win3 + WINB, t0 * RBM, vw1, lane, h);
+        ru8_w(u, wr3 + WT, 1, h, vk1, vk2);
+        if (h == 0) vm_wait<ru8::share(0, ru8::NPW, 0) + 8>();
+        else vm_wait<ru8::share(0, ru8::NPW, 1) + 8>();
+        int slot = 0;                       // ring slot of the current K-tile
+        for (int64_t t = t0; t < t1; ++t) {
+            const int64_t m0 = t * RBM;
+            const bool first = t == t0, more = t + 1 < t1;
+            sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
+                constexpr int kt = decltype(KT)::value;
+                // pre-barrier kt: at most step kt−1's pieces in flight (kt = 0: the prologue's or
+                // the previous tile's step 15, waited at the end of the previous iteration)
+                if constexpr (kt > 0) {
+                    if (h == 0) {
+                        if (first) {
+                            if (more) vm_wait<ru8::step_count(kt - 1, 0, true, true)>();
+                            else vm_wait<ru8::step_count(kt - 1, 0, true, false)>();
+                        } else {
+                            if (more) vm_wait<ru8::step_count(kt - 1, 0, false, true)>();
+                            else vm_wait<ru8::step_count(kt - 1, 0, false, false)>();
+                        }
+                    } else {
+                        if (first) {
+                            if (more) vm_wait<ru8::step_count(kt - 1, 1, true, true)>();
+                            else vm_wait<ru8::step_count(kt - 1, 1, true, false)>();
+                        } else {
+                            if (more) vm_wait<ru8::step_count(kt - 1, 1, false, true)>();
+                            else vm_wait<ru8::step_count(kt - 1, 1, false, false)>();
+                        }
+                    }
+                }
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                // step kt: window pieces, then W
+                if constexpr (kt <= 3) {
+                    if (!first) ru8_win<ru8::c1b_lo(kt), ru8::c1b_hi(kt)>(a, win3 + WINB, m0, vw1, lane, h);
+                }
+                if constexpr (kt >= 7 && kt <= 12) {
+                    if (more) ru8_win<ru8::c0_lo(kt - 7), ru8::c0_hi(kt - 7)>(a, win3, m0 + RBM, vw0, lane, h);
+                }
+                if constexpr (kt >= 14) {
+                    if (more) ru8_win<ru8::c1a_lo(kt - 14), ru8::c1a_hi(kt - 14)>(a, win3 + WINB, m0 + RBM, vw1, lane, h);
+                }
+                const int s2 = slot >= 1 ? slot - 1 : slot + 2;    // (slot + 2) % 3: K-tile kt−1's slot
+                if constexpr (kt <= 13) ru8_w(u, wr3 + s2 * WT, kt + 2, h, vk1, vk2);
+                else if (more) ru8_w(u, wr3 + s2 * WT, kt - 14, h, vk1, vk2);
+                slot = slot == 2 ? 0 : slot + 1;
+            });
+            // pre-barrier 0 of the next tile: at most step 15's pieces in flight
+            if (more) {
+                if (h == 0) vm_wait<ru8::step_count(15, 0, false, true)>();
+                else vm_wait<ru8::step_count(15, 1, false, true)>();
+            }
+        }
+        vm_wait<0>();
+        return;
+    }
+
+    // ---- MFMA waves 0-3: rows 64·wave .. +63 of each tile ----
+    if (tid < 128) {
+        psa2[tid] = a.sa[tid]; psib2[tid] = a.sib[tid];
+        psan[tid] = u.sa_next[tid]; psibn[tid] = u.sib_next[tid];
+        pb1[tid] = a.bias[tid]; pb2[tid] = u.b2[tid];
+    }
+    const int fr = lane & 15, fc = lane >> 4;
+    const bool odd = fc & 1;
+    const int wl[2] = {fr * 128 + ((fc ^ (fr & 7)) << 4), fr * 128 + (((4 + fc) ^ (fr & 7)) << 4)};
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int slot = 0;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t m0 = t * RBM;
+        bf16x8 yk[4][2];       // y_s k-steps 2, 3 of each row fragment, for K-tile 15
+        u32x4 xv[4][4];
+        // x (the residual) rows of row fragment i of this wave
+        // (row offsets computed at the load, from an opaque m0: hoisted to the tile start, the
+        // 16 offsets stayed live through the K loop and spilled)
+        auto load_x = [&](int i) __attribute__((always_inline)) {
+            int64_t mx = m0;
+            asm volatile("" : "+s"(mx));
+            const char *xb = (const char *)(u.x + mx * 128);
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+                const int r = (int)min((int64_t)(64 * wave + 16 * i + fr), a.M - 1 - mx);
+                const uint32_t off = (uint32_t)(r * 128 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8) * 2;
+                xv[i][jp] = *(const u32x4 *)(xb + off);
+            }
+        };
+        sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
+            constexpr int kt = decltype(KT)::value;
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char *tb = wr + slot * WT;
+            slot = slot == 2 ? 0 : slot + 1;
+            if constexpr (kt < 14) {
+                constexpr int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
+                int dl = a.dil;
+                asm volatile("" : "+s"(dl));
+                const int rb = 64 * wave + fr + tap * dl;
+                const char *wb = win + cc * WINB + rb * 128;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int xo = ((4 * ks + fc) ^ (rb & 7)) << 4;
+                    bf16x8 xf[4], wf[8];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8 *)(wb + i * 2048 + xo);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[ks]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+                }
+            } else if constexpr (kt == 14) {
+                // per row fragment: epilogue 1 (y_s = snake2(bf16(acc + b1)), the k=1 B fragments
+                // as in ru7_kernel), then its k=1 MFMAs over y_s k-steps 0, 1 (W2 half 0); k-steps
+                // 2, 3 wait for K-tile 15 — only one fragment's y_s is live at full width
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    // (parameter offsets opaque per fragment: hoisted, the 96 parameter values
+                    // would stay live across all four fragments)
+                    int pl = 4 * fc;
+                    asm volatile("" : "+v"(pl));
+                    uint2 yv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int n = 16 * j + pl;
+                        float b[4];
+                        unpack4(*(const uint2 *)(pb1 + n), b);
+                        const float4 sa = *(const float4 *)(psa2 + n), sb = *(const float4 *)(psib2 + n);
+                        const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
+                        float o[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + b[r]), sav[r], sbv[r]);
+                        yv[j] = pack4(o);
+                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+                    bf16x8 y[4];
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4)
+                        y[s4] = __builtin_bit_cast(bf16x8, make_uint4(yv[2 * s4].x, yv[2 * s4].y, yv[2 * s4 + 1].x,
+                                                                       yv[2 * s4 + 1].y));
+                    yk[i][0] = y[2];
+                    yk[i][1] = y[3];
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) {
+                        bf16x8 wf[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[ks]);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], y[ks], acc[i][j], 0, 0, 0);
+                    }
+                }
+            } else {
+                load_x(0);
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    bf16x8 wf[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[ks]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], yk[i][ks], acc[i][j], 0, 0, 0);
+                }
+            }
+        });
+        // epilogue 2: x' = x + bf16(acc + b2) (raw, optional) and snake_next(x') → out_s
+        int64_t me = m0;
+        asm volatile("" : "+s"(me));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < 3) load_x(i + 1);     // lands during fragment i's epilogue
+            int pl2 = (odd ? 16 : 0) + (fc >> 1) * 8;
+            asm volatile("" : "+v"(pl2));
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+                const int n = 32 * jp + pl2;
+                float bb[8];
+                unpack8(*(const uint4 *)(pb2 + n), bb);
+                const float4 a0 = *(const float4 *)(psan + n), a1 = *(const float4 *)(psan + n + 4);
+                const float4 s0 = *(const float4 *)(psibn + n), s1 = *(const float4 *)(psibn + n + 4);
+                const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                float o[8], rr[8], sn[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                acc[i][2 * jp] = f32x4{0.f, 0.f, 0.f, 0.f};
+                acc[i][2 * jp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                unpack8(make_uint4(xv[i][jp].x, xv[i][jp].y, xv[i][jp].z, xv[i][jp].w), rr);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+                    sn[r] = snake1(o[r], av[r], sv[r]);
+                }
+                const int64_t m = me + 64 * wave + 16 * i + fr;
+                if (m < a.M) {
+                    if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
+                    *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+                }
+            }
+        }
+    }
+}
+
 __global__ void permute_k1_kernel(const bf16_t *w, bf16_t *wp, int n_rows) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n_rows * 128) return;
@@ -1355,6 +1682,15 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
     const ConvArgs &a = u.c1;
     if (a.Cin != 128 || a.N != 128 || a.taps != 7 || !a.zero || !a.bias || !a.sa) return fail(-1, "resunit128: args");
     if (u.x == u.out_s || a.in == u.out_s) return fail(-1, "resunit128: out_s must not alias x / x_s");
+    if (knobs().ru7 == 2 && u.W2p && u.in_zero_pad && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
+        const int64_t nt = (a.M + ru8::BM - 1) / ru8::BM;
+        const int nb = (int)std::min<int64_t>(nt, (int64_t)num_cus_conv());
+        HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * 128), 0, (size_t)kActPadRows * 256, s));
+        if (u.keep_raw) ru8_kernel<true><<<nb, 384, 0, s>>>(u, nt);
+        else ru8_kernel<false><<<nb, 384, 0, s>>>(u, nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (use_ru7() && u.W2p && u.in_zero_pad && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
         const int64_t nt = (a.M + ru::BM - 1) / ru::BM;
         const int nb = (int)std::min<int64_t>(nt, 2 * (int64_t)num_cus_conv());

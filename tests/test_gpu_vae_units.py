@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from acehip import _ffi as ff
+from conftest import set_knob
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-2
@@ -102,11 +103,27 @@ def test_vae_conv_unit(gpu_device, kind, Cin, Cout, k, stride, dil, L, raw, use_
         assert rel_l2(out_s, ys) < TOL, ("snake", rel_l2(out_s, ys))
 
 
-@pytest.mark.parametrize("dil,L,keep", [(1, 3000, True), (3, 5000, False), (9, 70000, True), (9, 131, True)])
-def test_vae_resunit_c128(gpu_device, dil, L, keep):
-    """The persistent C = 128 residual unit (ru7_kernel) vs the torch composition
-    x + conv2(snake2(conv1(snake1(x)) + b1)) + b2 and snake_next of that; L = 70000 gives
-    ≥ 2 tiles per block (the cross-tile pipeline), L = 131 a ragged single partial tile."""
+def _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep):
+    C = x.shape[1]
+    x_out = torch.empty(L, C, device=x.device, dtype=torch.bfloat16) if keep else None
+    xs_out = torch.empty(L, C, device=x.device, dtype=torch.bfloat16)
+    ff.check(ff.lib().acehip_vae_resunit(ff.ptr(x), ff.ptr(x_s), L, C, dil, ff.ptr(w1), ff.ptr(bb1), ff.ptr(a2),
+                                         ff.ptr(be2), ff.ptr(w2), ff.ptr(bb2), ff.ptr(an), ff.ptr(ben),
+                                         ff.ptr(x_out), ff.ptr(xs_out), ff.stream_ptr()), "vae_resunit")
+    torch.cuda.synchronize()
+    return x_out, xs_out
+
+
+@pytest.mark.parametrize("ru", ["1", "2"])
+@pytest.mark.parametrize("dil,L,keep", [(1, 3000, True), (3, 5000, False), (9, 70000, True), (9, 131, True),
+                                        (9, 600000, True)])
+def test_vae_resunit_c128(gpu_device, monkeypatch, dil, L, keep, ru):
+    """The persistent C = 128 residual unit (ACEHIP_RU7=1: ru7_kernel, 128-row tiles; 2:
+    ru8_kernel, 256-row tiles with DMA helper waves) vs the torch composition
+    x + conv2(snake2(conv1(snake1(x)) + b1)) + b2 and snake_next of that; L = 70000 / 600000
+    give ≥ 2 tiles per block (the cross-tile pipeline), L = 131 a ragged single partial tile.
+    Both kernels accumulate in the same order, so ru8 must equal ru7 bit for bit."""
+    set_knob(monkeypatch, "ACEHIP_RU7", ru)
     C = 128
     g = torch.Generator(device=gpu_device).manual_seed(dil * 100 + L)
     x = _bf(torch.randn(L, C, device=gpu_device, generator=g))
@@ -118,12 +135,13 @@ def test_vae_resunit_c128(gpu_device, dil, L, keep):
     w2 = _bf(torch.randn(C, C, 1, device=gpu_device, generator=g) / math.sqrt(C))
     bb2 = _bf(torch.randn(C, device=gpu_device, generator=g) * 0.1)
     an, ben = _bf(torch.randn(C, device=gpu_device, generator=g) * 0.3), _bf(torch.randn(C, device=gpu_device, generator=g) * 0.3)
-    x_out = torch.empty(L, C, device=gpu_device, dtype=torch.bfloat16) if keep else None
-    xs_out = torch.empty(L, C, device=gpu_device, dtype=torch.bfloat16)
-    ff.check(ff.lib().acehip_vae_resunit(ff.ptr(x), ff.ptr(x_s), L, C, dil, ff.ptr(w1), ff.ptr(bb1), ff.ptr(a2),
-                                         ff.ptr(be2), ff.ptr(w2), ff.ptr(bb2), ff.ptr(an), ff.ptr(ben),
-                                         ff.ptr(x_out), ff.ptr(xs_out), ff.stream_ptr()), "vae_resunit")
-    torch.cuda.synchronize()
+    x_out, xs_out = _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep)
+    if ru == "2":
+        set_knob(monkeypatch, "ACEHIP_RU7", "1")
+        x7, xs7 = _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep)
+        assert torch.equal(xs_out, xs7), "ru8 out_s != ru7"
+        if keep:
+            assert torch.equal(x_out, x7), "ru8 x != ru7"
     y = F.conv1d(x_s.float().t()[None], w1.float(), bb1.float(), padding=3 * dil, dilation=dil)[0].t()
     y = snake(y, a2, be2)
     y = F.conv1d(y.t()[None], w2.float(), bb2.float())[0].t()
