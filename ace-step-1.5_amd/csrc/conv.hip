@@ -1096,12 +1096,26 @@ __device__ __forceinline__ void sfor(F &&f) {     // compile-time unrolled loop 
         sfor<I0 + 1, I1>(f);
     }
 }
+#ifndef RU8_D
+#define RU8_D 2            // W ring distance: W(kt + D) issued behind barrier kt (D + 1 slots)
+#endif
 namespace ru8 {
-constexpr int BM = 256, WROWS = 310, WINB = WROWS * 128, WT = 128 * 128, PAR = 2560, NSLOT = 3;
+#ifndef RU8_PIPE
+#define RU8_PIPE 0         // 1: MFMA waves read K-tile kt+1's k-step 0 during K-tile kt (needs D = 3)
+#endif
+constexpr int D = RU8_D;
+constexpr bool PIPE = RU8_PIPE != 0;
+constexpr int LA = PIPE ? 1 : 0;   // barrier kt publishes W(kt + LA)
+constexpr int BM = 256, WROWS = 310, WINB = WROWS * 128, WT = 128 * 128, PAR = 2560, NSLOT = D + 1;
+static_assert(D >= 2 && D <= 3, "W ring distance");
+static_assert(!PIPE || D == 3, "the pipelined K loop reads one K-tile ahead: W distance 3");
 constexpr int LDS = PAR + 2 * WINB + NSLOT * WT;
 constexpr int NPW = (WROWS + 7) / 8;   // 39 window pieces (8 rows) per chunk; the last is 6 rows
 static_assert(LDS <= 160 * 1024, "LDS");
 static_assert(BM + 54 <= WROWS, "halo of dilation 9");
+// (chunk 0 of the next tile, steps 7-12, is issued before W(0'), step 16 − D; chunk 1's pieces of
+// steps 0-3 before W(7), step 7 − D — so waiting for a K-tile's W also covers its window chunk)
+static_assert(16 - D > 12 && 7 - D > 3, "window pieces ordered before the W that guards them");
 // window piece ranges per helper step: chunk 0 of the next tile over steps 7-12; chunk 1 of the
 // next tile over steps 14-15 (pieces 0-13) and of the current one over steps 0-3 (14-38)
 __host__ __device__ constexpr int c0_lo(int s) { return s == 0 ? 0 : s == 1 ? 7 : s == 2 ? 14 : s == 3 ? 20 : s == 4 ? 26 : 33; }
@@ -1119,7 +1133,23 @@ __host__ __device__ constexpr int step_count(int s, int h, bool first, bool more
     if (s <= 3 && !first) n += share(c1b_lo(s), c1b_hi(s), h);
     if (s >= 7 && s <= 12 && more) n += share(c0_lo(s - 7), c0_hi(s - 7), h);
     if (s >= 14 && more) n += share(c1a_lo(s - 14), c1a_hi(s - 14), h);
-    if (s <= 13 || more) n += 8;
+    if (s + D <= 15 || more) n += 8;
+    return n;
+}
+// pieces helper h may leave in flight before barrier kt: everything issued after W(kt) (issued in
+// step kt − D, a step of the previous tile when negative, or by the first tile's prologue:
+// chunk 0, W(0), chunk 1, W(1) … W(D − 1))
+// (PIPE: W(kt + 1), which the MFMA waves start reading behind barrier kt)
+__host__ __device__ constexpr int allowed(int kt, int h, bool first, bool more) {
+    const int need = kt + LA;
+    int n = 0;
+    if (first && need < D) {
+        n = (D - 1 - need) * 8 + (need == 0 ? share(0, NPW, h) : 0);
+        for (int s = 0; s < kt; ++s) n += step_count(s, h, true, more);
+        return n;
+    }
+    for (int s = need - D + 1; s < kt; ++s)
+        n += s >= 0 ? step_count(s, h, first, more) : step_count(s + 16, h, false, true);
     return n;
 }
 }  // namespace ru8
@@ -1183,38 +1213,34 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
         const int l3 = lane >> 3, lc = ((lane & 7) ^ l3) * 16;
         const uint32_t vw0 = l3 * 256 + lc, vw1 = vw0 + 128;          // window chunk 0 / 1
         const uint32_t vk1 = l3 * 1792 + lc, vk2 = l3 * 256 + lc;       // W1 / W2 rows
-        // prologue: chunk 0, W(0), chunk 1, W(1); barrier 0 needs chunk 0 and W(0)
+        // prologue: chunk 0, W(0), chunk 1, W(1) … W(D − 1)
         ru8_win<0, ru8::NPW>(a, win3, t0 * RBM, vw0, lane, h);
         ru8_w(u, wr3, 0, h, vk1, vk2);
         ru8_win<0, ru8::NPW>(a, win3 + WINB, t0 * RBM, vw1, lane, h);
-        ru8_w(u, wr3 + WT, 1, h, vk1, vk2);
-        if (h == 0) vm_wait<ru8::share(0, ru8::NPW, 0) + 8>();
-        else vm_wait<ru8::share(0, ru8::NPW, 1) + 8>();
+#pragma unroll
+        for (int k = 1; k < ru8::D; ++k) ru8_w(u, wr3 + k * WT, k, h, vk1, vk2);
         int slot = 0;                       // ring slot of the current K-tile
         for (int64_t t = t0; t < t1; ++t) {
             const int64_t m0 = t * RBM;
             const bool first = t == t0, more = t + 1 < t1;
             sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
                 constexpr int kt = decltype(KT)::value;
-                // pre-barrier kt: at most step kt−1's pieces in flight (kt = 0: the prologue's or
-                // the previous tile's step 15, waited at the end of the previous iteration)
-                if constexpr (kt > 0) {
-                    if (h == 0) {
-                        if (first) {
-                            if (more) vm_wait<ru8::step_count(kt - 1, 0, true, true)>();
-                            else vm_wait<ru8::step_count(kt - 1, 0, true, false)>();
-                        } else {
-                            if (more) vm_wait<ru8::step_count(kt - 1, 0, false, true)>();
-                            else vm_wait<ru8::step_count(kt - 1, 0, false, false)>();
-                        }
+                // pre-barrier kt: W(kt) and everything issued before it landed
+                if (h == 0) {
+                    if (first) {
+                        if (more) vm_wait<ru8::allowed(kt, 0, true, true)>();
+                        else vm_wait<ru8::allowed(kt, 0, true, false)>();
                     } else {
-                        if (first) {
-                            if (more) vm_wait<ru8::step_count(kt - 1, 1, true, true)>();
-                            else vm_wait<ru8::step_count(kt - 1, 1, true, false)>();
-                        } else {
-                            if (more) vm_wait<ru8::step_count(kt - 1, 1, false, true)>();
-                            else vm_wait<ru8::step_count(kt - 1, 1, false, false)>();
-                        }
+                        if (more) vm_wait<ru8::allowed(kt, 0, false, true)>();
+                        else vm_wait<ru8::allowed(kt, 0, false, false)>();
+                    }
+                } else {
+                    if (first) {
+                        if (more) vm_wait<ru8::allowed(kt, 1, true, true)>();
+                        else vm_wait<ru8::allowed(kt, 1, true, false)>();
+                    } else {
+                        if (more) vm_wait<ru8::allowed(kt, 1, false, true)>();
+                        else vm_wait<ru8::allowed(kt, 1, false, false)>();
                     }
                 }
                 __builtin_amdgcn_s_barrier();
@@ -1229,16 +1255,11 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
                 if constexpr (kt >= 14) {
                     if (more) ru8_win<ru8::c1a_lo(kt - 14), ru8::c1a_hi(kt - 14)>(a, win3 + WINB, m0 + RBM, vw1, lane, h);
                 }
-                const int s2 = slot >= 1 ? slot - 1 : slot + 2;    // (slot + 2) % 3: K-tile kt−1's slot
-                if constexpr (kt <= 13) ru8_w(u, wr3 + s2 * WT, kt + 2, h, vk1, vk2);
-                else if (more) ru8_w(u, wr3 + s2 * WT, kt - 14, h, vk1, vk2);
-                slot = slot == 2 ? 0 : slot + 1;
+                const int sp = slot == 0 ? ru8::NSLOT - 1 : slot - 1;     // K-tile kt−1's slot = W(kt + D)'s
+                if constexpr (kt + ru8::D <= 15) ru8_w(u, wr3 + sp * WT, kt + ru8::D, h, vk1, vk2);
+                else if (more) ru8_w(u, wr3 + sp * WT, kt + ru8::D - 16, h, vk1, vk2);
+                slot = slot + 1 == ru8::NSLOT ? 0 : slot + 1;
             });
-            // pre-barrier 0 of the next tile: at most step 15's pieces in flight
-            if (more) {
-                if (h == 0) vm_wait<ru8::step_count(15, 0, false, true)>();
-                else vm_wait<ru8::step_count(15, 1, false, true)>();
-            }
         }
         vm_wait<0>();
         return;
@@ -1262,6 +1283,7 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
     for (int64_t t = t0; t < t1; ++t) {
         const int64_t m0 = t * RBM;
         bf16x8 yk[4][2];       // y_s k-steps 2, 3 of each row fragment, for K-tile 15
+        bf16x8 xp[4], wp[8];   // PIPE: the current K-tile's k-step-0 fragments
         u32x4 xv[4][4];
         // x (the residual) rows of row fragment i of this wave
         // (row offsets computed at the load, from an opaque m0: hoisted to the tile start, the
@@ -1281,9 +1303,59 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
             constexpr int kt = decltype(KT)::value;
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+            // (slot opaque: with 16 % NSLOT == 0 hipcc folds every K-tile's slot to a constant and
+            // hoists the 16 fragment bases out of the tile loop, where they spill)
+            asm volatile("" : "+s"(slot));
             const char *tb = wr + slot * WT;
-            slot = slot == 2 ? 0 : slot + 1;
-            if constexpr (kt < 14) {
+            slot = slot + 1 == ru8::NSLOT ? 0 : slot + 1;
+            if constexpr (kt < 14 && ru8::PIPE) {
+                // pipelined: this K-tile's k-step 0 fragments were read during the previous one
+                // (K-tile 0: here); k-step 1's are read now, and the next K-tile's k-step 0 behind
+                // this one's k-step-0 MFMAs (its W landed before this barrier: helpers wait one
+                // K-tile further ahead when PIPE)
+                int dl = a.dil;
+                asm volatile("" : "+s"(dl));
+                auto rbase = [&](int tap) __attribute__((always_inline)) { return 64 * wave + fr + tap * dl; };
+                constexpr int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
+                const int rb = rbase(tap);
+                const char *wb = win + cc * WINB + rb * 128;
+                if constexpr (kt == 0) {
+                    const int xo = (fc ^ (rb & 7)) << 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xp[i] = *(const bf16x8 *)(wb + i * 2048 + xo);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wp[j] = *(const bf16x8 *)(tb + j * 2048 + wl[0]);
+                }
+                bf16x8 xf[4], wf[8];
+                {
+                    const int xo = ((4 + fc) ^ (rb & 7)) << 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8 *)(wb + i * 2048 + xo);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[1]);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[j], xp[i], acc[i][j], 0, 0, 0);
+                if constexpr (kt < 13) {
+                    constexpr int cn = (kt + 1) >= 7 ? 1 : 0, tn = kt + 1 - 7 * cn;
+                    const int rn = rbase(tn);
+                    const char *wbn = win + cn * WINB + rn * 128;
+                    const char *tbn = wr + slot * WT;      // slot already advanced: K-tile kt+1's
+                    const int xo = (fc ^ (rn & 7)) << 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xp[i] = *(const bf16x8 *)(wbn + i * 2048 + xo);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wp[j] = *(const bf16x8 *)(tbn + j * 2048 + wl[0]);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+            } else if constexpr (kt < 14) {
                 constexpr int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
                 int dl = a.dil;
                 asm volatile("" : "+s"(dl));
