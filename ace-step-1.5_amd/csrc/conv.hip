@@ -1096,19 +1096,13 @@ __device__ __forceinline__ void sfor(F &&f) {     // compile-time unrolled loop 
         sfor<I0 + 1, I1>(f);
     }
 }
-#ifndef RU8_D
-#define RU8_D 2            // W ring distance: W(kt + D) issued behind barrier kt (D + 1 slots)
-#endif
 namespace ru8 {
-#ifndef RU8_PIPE
-#define RU8_PIPE 0         // 1: MFMA waves read K-tile kt+1's k-step 0 during K-tile kt (needs D = 3)
-#endif
-constexpr int D = RU8_D;
-constexpr bool PIPE = RU8_PIPE != 0;
-constexpr int LA = PIPE ? 1 : 0;   // barrier kt publishes W(kt + LA)
+// W ring distance: W(kt + D) is issued behind barrier kt into the slot of K-tile kt − 1 (D + 1
+// slots).  Measured (tools/ab_vae.py, one process, bit-identical): D = 3 (4 slots) 39.93 vs 39.90
+// ms per decode; D = 3 with the MFMA waves reading K-tile kt+1's k-step-0 fragments during
+// K-tile kt 40.61 (`profiles/r04ru8d_ab.log`) — W latency is not what bounds this kernel
+constexpr int D = 2;
 constexpr int BM = 256, WROWS = 310, WINB = WROWS * 128, WT = 128 * 128, PAR = 2560, NSLOT = D + 1;
-static_assert(D >= 2 && D <= 3, "W ring distance");
-static_assert(!PIPE || D == 3, "the pipelined K loop reads one K-tile ahead: W distance 3");
 constexpr int LDS = PAR + 2 * WINB + NSLOT * WT;
 constexpr int NPW = (WROWS + 7) / 8;   // 39 window pieces (8 rows) per chunk; the last is 6 rows
 static_assert(LDS <= 160 * 1024, "LDS");
@@ -1139,9 +1133,8 @@ __host__ __device__ constexpr int step_count(int s, int h, bool first, bool more
 // pieces helper h may leave in flight before barrier kt: everything issued after W(kt) (issued in
 // step kt − D, a step of the previous tile when negative, or by the first tile's prologue:
 // chunk 0, W(0), chunk 1, W(1) … W(D − 1))
-// (PIPE: W(kt + 1), which the MFMA waves start reading behind barrier kt)
 __host__ __device__ constexpr int allowed(int kt, int h, bool first, bool more) {
-    const int need = kt + LA;
+    const int need = kt;
     int n = 0;
     if (first && need < D) {
         n = (D - 1 - need) * 8 + (need == 0 ? share(0, NPW, h) : 0);
@@ -1283,7 +1276,6 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
     for (int64_t t = t0; t < t1; ++t) {
         const int64_t m0 = t * RBM;
         bf16x8 yk[4][2];       // y_s k-steps 2, 3 of each row fragment, for K-tile 15
-        bf16x8 xp[4], wp[8];   // PIPE: the current K-tile's k-step-0 fragments
         u32x4 xv[4][4];
         // x (the residual) rows of row fragment i of this wave
         // (row offsets computed at the load, from an opaque m0: hoisted to the tile start, the
@@ -1308,54 +1300,7 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
             asm volatile("" : "+s"(slot));
             const char *tb = wr + slot * WT;
             slot = slot + 1 == ru8::NSLOT ? 0 : slot + 1;
-            if constexpr (kt < 14 && ru8::PIPE) {
-                // pipelined: this K-tile's k-step 0 fragments were read during the previous one
-                // (K-tile 0: here); k-step 1's are read now, and the next K-tile's k-step 0 behind
-                // this one's k-step-0 MFMAs (its W landed before this barrier: helpers wait one
-                // K-tile further ahead when PIPE)
-                int dl = a.dil;
-                asm volatile("" : "+s"(dl));
-                auto rbase = [&](int tap) __attribute__((always_inline)) { return 64 * wave + fr + tap * dl; };
-                constexpr int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
-                const int rb = rbase(tap);
-                const char *wb = win + cc * WINB + rb * 128;
-                if constexpr (kt == 0) {
-                    const int xo = (fc ^ (rb & 7)) << 4;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) xp[i] = *(const bf16x8 *)(wb + i * 2048 + xo);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) wp[j] = *(const bf16x8 *)(tb + j * 2048 + wl[0]);
-                }
-                bf16x8 xf[4], wf[8];
-                {
-                    const int xo = ((4 + fc) ^ (rb & 7)) << 4;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8 *)(wb + i * 2048 + xo);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) wf[j] = *(const bf16x8 *)(tb + j * 2048 + wl[1]);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[j], xp[i], acc[i][j], 0, 0, 0);
-                if constexpr (kt < 13) {
-                    constexpr int cn = (kt + 1) >= 7 ? 1 : 0, tn = kt + 1 - 7 * cn;
-                    const int rn = rbase(tn);
-                    const char *wbn = win + cn * WINB + rn * 128;
-                    const char *tbn = wr + slot * WT;      // slot already advanced: K-tile kt+1's
-                    const int xo = (fc ^ (rn & 7)) << 4;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) xp[i] = *(const bf16x8 *)(wbn + i * 2048 + xo);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) wp[j] = *(const bf16x8 *)(tbn + j * 2048 + wl[0]);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
-            } else if constexpr (kt < 14) {
+            if constexpr (kt < 14) {
                 constexpr int cc = kt >= 7 ? 1 : 0, tap = kt - 7 * cc;
                 int dl = a.dil;
                 asm volatile("" : "+s"(dl));
@@ -1683,7 +1628,7 @@ bool use_convp(const ConvArgs &a, int phases) {
     return v == 1 || (v == 2 && a.taps == 1 && phases == 1);
 }
 
-// ACEHIP_RU7=0 keeps the C = 128 residual units on conv7_kernel<FUSED> (A/B knob)
+// C = 128 residual units: ACEHIP_RU7=2 (default) ru8_kernel, 1 ru7_kernel, 0 conv7_kernel<FUSED> (A/B)
 bool use_ru7() { return knobs().ru7 != 0; }
 
 int num_cus_conv() {

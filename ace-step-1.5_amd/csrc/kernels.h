@@ -26,7 +26,7 @@ struct Knobs {
     int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body
     int conv7 = 1;            // ACEHIP_CONV7: halo-staged k = 7 VAE convs
     int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
-    int ru7 = 1;              // ACEHIP_RU7: persistent C = 128 residual unit
+    int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
     unsigned gen = 0;
 };
 const Knobs &knobs();

@@ -37,7 +37,7 @@ Knobs read_env() {
     k.dit_graph = env_int("ACEHIP_DIT_GRAPH", 0);
     k.conv7 = env_int("ACEHIP_CONV7", 1);
     k.convp = env_int("ACEHIP_CONVP", 2);
-    k.ru7 = env_int("ACEHIP_RU7", 1);
+    k.ru7 = env_int("ACEHIP_RU7", 2);
     return k;
 }
 
