@@ -1,5 +1,5 @@
 #!/bin/bash
-# helper waves in the small-M tiles (variant 17, split-K with ACEHIP_GEMM_SKHELP=1)
+# helper waves in the small-M tiles (variant 17, split-K with ACEHIP_GEMM_SKHELP=1) — historical: the split-K helper switch was removed after this A/B (no gain)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_dit.py -k "gemm_variants or small" > gpurun_out/r04h2_tests.log 2>&1 || { tail -30 gpurun_out/r04h2_tests.log; exit 1; }
