@@ -1,7 +1,7 @@
 #!/bin/bash
+# (historical: the RU8_D / RU8_PIPE variants were removed after this A/B; DESIGN §3)
 # ru8 W ring distance 2 (tree) vs 3 (libacehip_d3.so) vs 3 + the pipelined K loop
 # (libacehip_d3p.so), all on ACEHIP_RU7=2: 240 s decode A/B in one process (bit-equality
-# (historical: the RU8_D / RU8_PIPE variants were removed after this A/B; DESIGN §3)
 # reported), then the ru7 / ru8 knob A/B on the tree library
 set -o pipefail
 mkdir -p gpurun_out
