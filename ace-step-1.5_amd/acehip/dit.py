@@ -366,7 +366,10 @@ class AceStepDiTBackend:
         enc_nc = ctx_nc = None
         acs = float(kw.get("audio_cover_strength", 1.0))
         if acs < 1.0:
-            enc_nc, _, ctx_nc = self._non_cover_condition(kw, ctx)
+            if kw.get("_non_cover") is not None:      # conditioned upstream (SongParallelPipeline)
+                enc_nc, ctx_nc = kw["_non_cover"]
+            else:
+                enc_nc, _, ctx_nc = self._non_cover_condition(kw, ctx)
         dtype, device = self.dtype, self.device
         ctx = ctx.to(device=device, dtype=dtype).contiguous()
         enc = enc.to(device=device, dtype=dtype)
@@ -382,6 +385,15 @@ class AceStepDiTBackend:
         costs["diffusion_per_step_time_cost"] = (t2 - t1) / max(n, 1)
         costs["total_time_cost"] = t2 - t0
         return {"target_latents": xt, "time_costs": costs}
+
+    def _noise(self, kw, shape):
+        """prepare_noise (base:1733-1770), or the ``_noise`` rows a song-parallel caller drew
+        for the whole batch on rank 0 (so an int seed's single batch generator is honoured)."""
+        if kw.get("_noise") is not None:
+            n = kw["_noise"]
+            assert tuple(n.shape) == tuple(shape), (tuple(n.shape), shape)
+            return n.to(device=self.device, dtype=self.dtype)
+        return prepare_noise(shape, self.device, self.dtype, kw.get("seed"))
 
     def _use_steps(self) -> bool:
         """Schedule-wide timestep MLPs (acehip_dit_set_timesteps) for the bf16 runtime;
@@ -410,7 +422,7 @@ class AceStepDiTBackend:
         use_adg = bool(kw.get("use_adg", False))
         t = base_schedule(infer_steps, shift, device, dtype,
                           kw.get("timesteps") if self.accepts_timesteps else None)
-        noise = prepare_noise((B, T, ctx.shape[-1] // 2), device, dtype, kw.get("seed"))
+        noise = self._noise(kw, (B, T, ctx.shape[-1] // 2))
         cns = float(kw.get("cover_noise_strength", 0.0))
         if cns > 0.0:
             tv = t[:-1].tolist()
@@ -468,7 +480,7 @@ class AceStepDiTBackend:
         dtype, device = self.dtype, self.device
         B, T = ctx.shape[0], ctx.shape[1]
         sched = turbo_schedule(float(kw.get("shift", 3.0)), kw.get("timesteps"))
-        noise = prepare_noise((B, T, ctx.shape[-1] // 2), device, dtype, kw.get("seed"))
+        noise = self._noise(kw, (B, T, ctx.shape[-1] // 2))
         cns = float(kw.get("cover_noise_strength", 0.0))
         if cns > 0.0:
             nearest = min(sched, key=lambda x: abs(x - (1.0 - cns)))

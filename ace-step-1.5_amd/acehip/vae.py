@@ -6,6 +6,8 @@ HIP kernels.  No CPU fallback: the library must load.
 """
 from __future__ import annotations
 
+import os
+
 from types import SimpleNamespace
 from typing import Dict, Optional
 
@@ -148,16 +150,24 @@ class OobleckBackend:
         ``chunk_size`` samples (default 30 s, 15 s on a GPU of ≤ 8 GB, vae_encode.py:46-53)
         comes back on the device whatever ``offload_latent_to_cpu`` says (vae_encode.py:62-68);
         longer ones are offloaded when it is set."""
-        del overlap
         if chunk_size is None:
-            mem_gb = torch.cuda.get_device_properties(self.device).total_memory / 1024 ** 3
+            # get_gpu_memory_gb (gpu_config.py:316-360): the MAX_CUDA_VRAM debug override first
+            try:
+                mem_gb = float(os.environ["MAX_CUDA_VRAM"])
+            except (KeyError, ValueError):
+                mem_gb = torch.cuda.get_device_properties(self.device).total_memory / 1024 ** 3
             chunk_size = 48000 * 15 if mem_gb <= 8 else 48000 * 30
+        if overlap is None:
+            overlap = 48000 * 2
         was_2d = audio.dim() == 2
         if was_2d:
             audio = audio.unsqueeze(0)
         if audio.dim() != 3 or audio.shape[1] != self.cfg.audio_channels:
             raise ValueError(f"acehip tiled_encode: expected [B, {self.cfg.audio_channels}, N] audio, "
                              f"got {tuple(audio.shape)}")
+        if audio.shape[-1] > chunk_size and chunk_size - 2 * overlap <= 0:
+            # the reference's chunked branch refuses a non-positive stride (vae_encode.py:70-72)
+            raise ValueError(f"chunk_size {chunk_size} must be > 2 * overlap {overlap}")
         z = self.encode_tensor(audio, sample=True)
         if was_2d:
             z = z.squeeze(0)

@@ -25,6 +25,10 @@ struct ConvArgs {
 // zero rows (of the widest stage, 2048 channels) kept in front of the VAE activation buffers:
 // the persistent residual-unit kernel reads the k=7 halo rows before the start from them
 constexpr int kActPadRows = 32;
+// rows past L that a C = 128 residual-unit window may read (ru8_kernel: a 310-row window from
+// m0 - 3·dil of the last 256-row tile, so up to L + 306): the back pad of every activation
+// buffer covers at least this many 128-channel rows whatever the widest stage is
+constexpr int kResWindowBackRows = 320;
 struct ResUnitArgs {
     ConvArgs c1;
     const bf16_t *W2, *b2;

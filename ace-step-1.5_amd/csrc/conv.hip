@@ -1107,6 +1107,7 @@ constexpr int LDS = PAR + 2 * WINB + NSLOT * WT;
 constexpr int NPW = (WROWS + 7) / 8;   // 39 window pieces (8 rows) per chunk; the last is 6 rows
 static_assert(LDS <= 160 * 1024, "LDS");
 static_assert(BM + 54 <= WROWS, "halo of dilation 9");
+static_assert(WROWS - 3 <= kResWindowBackRows, "the activation back pad covers the last tile's window");
 // (chunk 0 of the next tile, steps 7-12, is issued before W(0'), step 16 − D; chunk 1's pieces of
 // steps 0-3 before W(7), step 7 − D — so waiting for a K-tile's W also covers its window chunk)
 static_assert(16 - D > 12 && 7 - D > 3, "window pieces ordered before the W that guards them");

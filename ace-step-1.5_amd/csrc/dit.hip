@@ -338,7 +338,8 @@ int acehip_dit_create(int device, const acehip_dit_cfg *cfg, acehip_dit **out) {
     // (all 24 layers in one GEMM for a CFG song, one layer per GEMM at the 16 × 2048 maximum)
     {
         const size_t per_layer = Bc * Le * 2 * kvd * 2;
-        h->kv_group = (int)std::max<size_t>(1, std::min<size_t>((size_t)L, ((size_t)256 << 20) / per_layer));
+        const size_t bound = (size_t)knobs().kv_group_kib << 10;      // 256 MiB by default
+        h->kv_group = (int)std::max<size_t>(1, std::min<size_t>((size_t)L, bound / per_layer));
     }
     h->E = A(Bc * Le * D); h->KVtmp = A(Bc * Le * 2 * kvd * (size_t)h->kv_group);
     h->cnull = A((size_t)L * D); h->vnull = A(qd);
@@ -483,6 +484,26 @@ int acehip_dit_set_weight(acehip_dit *h, const char *name, const void *ptr, int 
     return fail(ACEHIP_E_ARG, "dit_set_weight: unhandled pack kind");
 }
 
+// Buffers of acehip_dit_set_timesteps for `cap` steps: allocated at finalize for kTsCap
+// steps (every schedule the reference builds: ≤ 60 base/sft steps, ≤ 20 turbo), grown only
+// by a longer schedule (the header documents that exception to "no allocation in calls").
+static constexpr int kTsCap = 64;
+static int alloc_timesteps(acehip_dit *h, int n_steps) {
+    for (bf16_t *p : {h->ts_temb, h->ts_proj, h->ts_scratch})
+        if (p) (void)hipFree(p);
+    h->ts_temb = h->ts_proj = h->ts_scratch = nullptr;
+    h->ts_cap = h->ts_n = 0;
+    const int D = h->D;
+    const int cap = std::max(n_steps, kTsCap);
+    // scratch: emb [2][cap][256], h1 [cap][D], temb_e [2][cap][D], proj_e [2][cap][6D]
+    const size_t scratch = (size_t)cap * (2 * 256 + D + 2 * D + 2 * 6 * D);
+    HIP_TRY(hipMalloc(&h->ts_temb, (size_t)cap * D * 2));
+    HIP_TRY(hipMalloc(&h->ts_proj, (size_t)cap * 6 * D * 2));
+    HIP_TRY(hipMalloc(&h->ts_scratch, scratch * 2));
+    h->ts_cap = cap;
+    return 0;
+}
+
 int acehip_dit_finalize(acehip_dit *h) {
     if (!h) return fail(ACEHIP_E_ARG, "null handle");
     HIP_TRY(hipSetDevice(h->device));
@@ -494,6 +515,7 @@ int acehip_dit_finalize(acehip_dit *h) {
     if (h->F % 32) return fail(ACEHIP_E_ARG, "intermediate must be a multiple of 32");
     int rc = h->f32 ? build_rope_f32(h) : build_rope(h);
     if (rc) return rc;
+    if (!h->f32 && h->ts_cap < kTsCap && (rc = alloc_timesteps(h, kTsCap))) return rc;
     HIP_TRY(hipDeviceSynchronize());
     h->finalized = true;
     return 0;
@@ -601,19 +623,10 @@ int acehip_dit_set_timesteps(acehip_dit *h, const float *t, const float *t_r, in
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     const int D = h->D;
-    if (n_steps > h->ts_cap) {
+    if (n_steps > h->ts_cap) {                 // only schedules longer than kTsCap steps
         HIP_TRY(hipStreamSynchronize(s));
-        for (bf16_t *p : {h->ts_temb, h->ts_proj, h->ts_scratch})
-            if (p) (void)hipFree(p);
-        h->ts_temb = h->ts_proj = h->ts_scratch = nullptr;
-        h->ts_cap = h->ts_n = 0;
-        const int cap = std::max(n_steps, 64);
-        // scratch: emb [2][cap][256], h1 [cap][D], temb_e [2][cap][D], proj_e [2][cap][6D]
-        const size_t scratch = (size_t)cap * (2 * 256 + D + 2 * D + 2 * 6 * D);
-        HIP_TRY(hipMalloc(&h->ts_temb, (size_t)cap * D * 2));
-        HIP_TRY(hipMalloc(&h->ts_proj, (size_t)cap * 6 * D * 2));
-        HIP_TRY(hipMalloc(&h->ts_scratch, scratch * 2));
-        h->ts_cap = cap;
+        int rc = alloc_timesteps(h, n_steps);
+        if (rc) return rc;
     }
     const size_t cap = h->ts_cap;
     bf16_t *emb[2] = {h->ts_scratch, h->ts_scratch + cap * 256};

@@ -27,6 +27,7 @@ struct Knobs {
     int conv7 = 1;            // ACEHIP_CONV7: halo-staged k = 7 VAE convs
     int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
     int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
+    int kv_group_kib = 262144; // ACEHIP_KV_GROUP_KIB: cross-K/V scratch bound at dit_create (tests force small groups)
     unsigned gen = 0;
 };
 const Knobs &knobs();

@@ -38,6 +38,8 @@ Knobs read_env() {
     k.conv7 = env_int("ACEHIP_CONV7", 1);
     k.convp = env_int("ACEHIP_CONVP", 2);
     k.ru7 = env_int("ACEHIP_RU7", 2);
+    k.kv_group_kib = env_int("ACEHIP_KV_GROUP_KIB", 262144);
+    if (k.kv_group_kib <= 0) k.kv_group_kib = 262144;
     return k;
 }
 

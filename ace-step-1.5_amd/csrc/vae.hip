@@ -243,8 +243,8 @@ int acehip_vae_create(int device, const acehip_vae_cfg *cfg, acehip_vae **out) {
     // front and as many addressable rows behind: the persistent residual-unit kernel reads its
     // halo rows before the start from the front ones and whole windows past the end from the
     // back ones (resunit128 zeroes the first kActPadRows rows past L before each launch)
-    const size_t pad = (size_t)kActPadRows * std::max(h->dec[0].cin, cfg->encoder_hidden * cm[n]) * 2;
-    static_assert(kActPadRows * 2048 * 2 >= 192 * 128 * 2, "back pad covers a C = 128 window");
+    const size_t pad = std::max((size_t)kActPadRows * std::max(h->dec[0].cin, cfg->encoder_hidden * cm[n]) * 2,
+                                (size_t)kResWindowBackRows * 128 * 2);
     bf16_t **bufs[3] = {&h->X, &h->P, &h->Q};
     for (bf16_t **b : bufs) {
         char *p = (char *)valloc(h, (size_t)mx * 2 + 2 * pad);
@@ -519,7 +519,7 @@ int acehip_vae_resunit(const void *x, const void *x_s, int64_t L, int C, int dil
     if (!zero) return fail(ACEHIP_E_OOM, "vae_resunit: zero page");
     Tmp t;
     // the decoder's activation layout: kActPadRows zero rows in front, addressable rows behind
-    const size_t rowb = (size_t)C * 2, pad = (size_t)kActPadRows * 2048 * 2;
+    const size_t rowb = (size_t)C * 2, pad = std::max((size_t)kActPadRows * 2048 * 2, (size_t)kResWindowBackRows * 128 * 2);
     char *xs_pad = (char *)t.get((size_t)L * rowb + 2 * pad);
     bf16_t *xr = (bf16_t *)t.get((size_t)L * rowb);
     ResU r;

@@ -13,7 +13,8 @@ Multi-GPU (``--gpus N``): one song per GPU per step (song-parallel, SURVEY
 §8e), one process per GPU.  Under a launcher (torchrun sets WORLD_SIZE) the
 ranks come from the environment and must equal N; started plainly with N > 1,
 bench.py spawns the N ranks itself (``acehip.distributed.launch_local``, before
-anything touches the GPU).  Conditioning is broadcast from rank 0 over RCCL, no
+anything touches the GPU).  Rank 0 conditions each step's batch once and scatters each
+rank its song (acehip.distributed.SongParallelPipeline) over RCCL, no
 collective inside the timed work; value = max-over-ranks time ÷ all songs.
 ``--dry-run`` runs the same harness on CPU ranks over gloo with a stand-in song
 (the multi-rank CPU test drives it).
@@ -253,14 +254,16 @@ def main():
     prep = None
     if not args.no_condition:
         # lyric + timbre + text encoders on the HIP path; Lenc = lyric + 1 timbre + text
-        ce = ConditionEncoder(cfg, local, max_batch=1, max_lyric=args.lyric_len, max_refs=1, max_ref_frames=750)
+        ce = ConditionEncoder(cfg, local, max_batch=world, max_lyric=args.lyric_len, max_refs=world,
+                              max_ref_frames=750)
         ce.load(synth_condenc_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch"))
         prep = HipPrepareCondition(ce)
         args.lenc = args.lyric_len + 1 + args.text_len
         # the Qwen3-Embedding-0.6B text encoder (infer_text_embeddings / infer_lyric_embeddings,
         # conditioning_embed.py:71-79): 28 causal layers for the text tokens, the table for lyrics
         te_cfg = DiTConfig(**TextEncoder.QWEN3_06B)
-        te = TextEncoder(te_cfg, local, max_batch=1, max_tokens=max(args.text_len, 64), overlap=not args.no_overlap)
+        te = TextEncoder(te_cfg, local, max_batch=world, max_tokens=max(args.text_len, 64),
+                         overlap=not args.no_overlap)
         te.load(synth_text_encoder_weights(te_cfg, QWEN3_VOCAB, seed=0, mode="bench", device=dev,
                                            dtype=torch.bfloat16, backend="torch"))
     be = AceStepDiTBackend(rt, null, is_turbo=args.turbo, prepare_condition=prep)
@@ -320,47 +323,58 @@ def main():
         span_mask = torch.zeros(1, T, 64, device=dev, dtype=torch.bfloat16)
         span_mask[:, span[0]:span[1]] = 1
 
-    dit_s_total = [0.0]
-    vae_s_total = [0.0]
+    if span is not None and world > 1:
+        raise SystemExit("bench.py: --repaint is the 1-GPU config 5 (SURVEY §8d); run it with --gpus 1")
+    # song-parallel: rank 0 conditions the step's batch of `world` songs once
+    # (text encoder + prepare_condition in one batched pass) and draws the batch noise, each rank
+    # gets its song by scatter, runs generate_audio + the VAE decode on its own GPU, and the
+    # latents return to rank 0; at world 1 the scatter / gather are the identity
+    pipe = D.SongParallelPipeline(be, vae, device=dev, gather_wav=False)
+    pipe.timing = True
 
-    def song(seed):
+    def batch_kwargs(seeds):
+        Bw = len(seeds)
+        if args.no_condition:
+            return dict(encoder_hidden_states=enc.expand(Bw, -1, -1).contiguous(),
+                        context_latents=ctx.expand(Bw, -1, -1).contiguous(), seed=seeds)
+        kw = {k: v.expand(Bw, *v.shape[1:]).contiguous() for k, v in cond_kw.items()}
+        kw["refer_audio_order_mask"] = torch.arange(Bw, device=dev, dtype=torch.long)
+        kw.update(text_hidden_states=te(input_ids=text_ids.expand(Bw, -1).contiguous(),
+                                        lyric_attention_mask=None).last_hidden_state,
+                  lyric_hidden_states=te.embed_tokens(lyric_ids.expand(Bw, -1).contiguous()), seed=seeds)
+        return kw
+
+    def song(idx, warm=False):
         e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e2 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        if not args.no_condition:
-            cond_kw.update(text_hidden_states=te(input_ids=text_ids, lyric_attention_mask=None).last_hidden_state,
-                           lyric_hidden_states=te.embed_tokens(lyric_ids))
+        seeds = [(10_000 + r * 100 + idx) if warm else (r * 1000 + idx) for r in range(world)]
         if span is not None:
             # vae.encode(x).latent_dist.sample() (vae_encode.py:65), then the repaint source:
             # encoded target with silence inside the span + chunk mask of the span
-            # (conditioning_masks.py:67-83)
-            # through the handler seam as the reference calls it (batch_prep.py:63-76:
-            # tiled_encode(audio, offload_latent_to_cpu=True) → .to(device) → transpose)
+            # (conditioning_masks.py:67-83), through the handler seam as the reference calls it
+            # (batch_prep.py:63-76: tiled_encode(audio, offload_latent_to_cpu=True) → .to(device))
             z = vae.tiled_encode(src_wav, offload_latent_to_cpu=True).to(dev).transpose(1, 2)
             src_r = z.clone()
             src_r[:, span[0]:span[1]] = src[:, span[0]:span[1]]
             cond_kw.update(src_latents=src_r.contiguous(), chunk_masks=span_mask)
-        res = be.generate_audio(**cond_kw, infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance,
-                                shift=args.shift, seed=seed, infer_method="ode")
-        e1.record()
-        if vae is not None:
-            wav = vae.decode_tensor(res["target_latents"].transpose(1, 2))
-            # decode output guard (generate_music_decode.py:193-195) + the product's default
-            # normalize_audio(-1 dBFS) (inference.py:674-679), fused in one HIP pass pair
-            vae.postprocess_(wav, normalization_db=-1.0)
-        e2.record()
+        sampler = dict(infer_steps=args.infer_steps, diffusion_guidance_sale=args.guidance, shift=args.shift,
+                       infer_method="ode")
+        if rank == 0:
+            pipe.generate(**batch_kwargs(seeds), **sampler)
+        else:
+            pipe.serve_one()
+        e1, e2 = pipe.last_events
         return e0, e1, e2
 
     for i in range(args.warmup):
-        song(10_000 + rank * 100 + i)
+        song(i, warm=True)
     torch.cuda.synchronize()
     # inside the timed region only the roofline kernel carries events
     rt.profile(True, kinds=["gemm_swiglu"])
     D.barrier(dev)
     torch.cuda.synchronize()
     t0 = time.time()
-    evs = [song(rank * 1000 + i) for i in range(args.steps)]
+    evs = [song(i) for i in range(args.steps)]
     torch.cuda.synchronize()
     D.barrier(dev)
     elapsed = time.time() - t0
@@ -368,7 +382,7 @@ def main():
     prof = rt.profile_read()
     # per-kernel breakdown from one extra, untimed song with every family timed
     rt.profile(True)
-    song(rank * 1000 + 999)
+    song(999)
     torch.cuda.synchronize()
     prof_all = rt.profile_read()
     rt.profile(False)

@@ -8,8 +8,15 @@
  * device-resident buffers (e.g. torch.Tensor.data_ptr()); the library owns the
  * packed weights, the cross-attention K/V cache and the workspace (sized at
  * create time from the max_* fields).  Nothing is allocated inside
- * forward/decode/encode/sampler calls.  Work is enqueued on the caller's
- * stream (hipStream_t passed as void*); no entry point synchronises the host.
+ * forward/decode/encode calls.  Two calls allocate, once, outside the hot loop:
+ *   - acehip_sampler_apg_euler keeps its norm partials in a library-owned
+ *     workspace per (device, stream), allocated on the first call on that stream
+ *     and grown (hipFree + hipMalloc) only when a larger B*T arrives;
+ *   - acehip_dit_set_timesteps uses buffers allocated at finalize for 64 steps;
+ *     a longer schedule (the reference builds <= 60) synchronises the stream and
+ *     grows them once.
+ * Work is enqueued on the caller's stream (hipStream_t passed as void*); apart from
+ * that growth no entry point synchronises the host.
  *
  * Threading: a handle is bound to one device and is not re-entrant; every
  * entry point calls hipSetDevice(handle->device) first because callers (the

@@ -875,3 +875,35 @@ def test_splitk_epilogue_fused_into_consumers(gpu_device, monkeypatch, mode):
         out = fused.float().cpu()
         assert rel_l2(out, ref) <= TOL_REL and cosine(out, ref) >= TOL_COS
     rt.close()
+
+
+def test_cross_kv_grouped_gemms(gpu_device, monkeypatch):
+    """set_condition's cross K/V projections run as GEMMs over groups of kv_group layers (the
+    group bounded by a scratch budget: at the production handle's max_Bc 16 x max_Lenc 2048 it
+    is 2 layers per GEMM).  ACEHIP_KV_GROUP_KIB shrinks the budget so a tiny 5-layer handle runs
+    groups of 2, 2, 1 (ldkv = G·2·kvd with a partial last group) — the forward must equal the
+    one-group handle's and the oracle's."""
+    from acehip.dit import DiTRuntime
+    cfg = DiTConfig.tiny(layers=5, window=8)
+    W = synth_dit_weights(cfg, seed=17, mode="parity")
+    g = torch.Generator().manual_seed(17)
+    B, T, Le = 2, 60, 32
+    xt = torch.randn(B, T, 64, generator=g).bfloat16().to(gpu_device)
+    ctx = torch.randn(B, T, 128, generator=g).bfloat16().to(gpu_device)
+    enc = torch.randn(B, Le, cfg.hidden_size, generator=g).bfloat16().to(gpu_device)
+    t = torch.tensor([0.4375, 0.8125], dtype=torch.float32, device=gpu_device)
+    outs = []
+    for kib in (None, 64):                       # per layer: 2·32·2·128·2 B = 32 KiB → groups of 2
+        if kib:
+            set_knob(monkeypatch, "ACEHIP_KV_GROUP_KIB", kib)
+        rt = _runtime(cfg, W, gpu_device, max_S=32, max_Bc=2, max_Lenc=Le)
+        rt.set_condition(enc)
+        outs.append(rt.forward(xt, ctx, t).float().cpu())
+        torch.cuda.synchronize()
+        rt.close()
+    Wb = {k: v.bfloat16() for k, v in W.items()}
+    with torch.no_grad():
+        ref = dit_oracle.dit_forward(Wb, cfg, xt.cpu(), t.cpu().bfloat16(), t.cpu().bfloat16(), enc.cpu(),
+                                     ctx.cpu()).float()
+    assert rel_l2(outs[1], outs[0]) < 1e-3, rel_l2(outs[1], outs[0])
+    assert rel_l2(outs[1], ref) <= TOL_REL and cosine(outs[1], ref) >= TOL_COS

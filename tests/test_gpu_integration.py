@@ -313,10 +313,11 @@ def test_install_drives_handler_calls(gpu_device, installed):
     zs = h.tiled_encode(audio)
     assert zs.is_cuda and zs.shape == (2, 64, T) and zs.dtype == torch.bfloat16
     torch.manual_seed(5)
-    zc = h.tiled_encode(audio, chunk_size=n - 1)                # "long" source: offloaded
+    ov = 1920                                                    # stride = chunk - 2·overlap > 0
+    zc = h.tiled_encode(audio, chunk_size=n - 1, overlap=ov)    # "long" source: offloaded
     assert zc.device.type == "cpu" and torch.equal(zc, zs.cpu())
     torch.manual_seed(5)
-    zg = h.tiled_encode(audio, chunk_size=n - 1, offload_latent_to_cpu=False)
+    zg = h.tiled_encode(audio, chunk_size=n - 1, overlap=ov, offload_latent_to_cpu=False)
     assert zg.is_cuda and torch.equal(zg.cpu(), zc)
     torch.manual_seed(5)
     eps = torch.randn(2, 64, T, device=gpu_device, dtype=torch.bfloat16)
@@ -327,6 +328,8 @@ def test_install_drives_handler_calls(gpu_device, installed):
     assert not torch.equal(zg, mean)                             # a sample, not the mode
     z1 = h.tiled_encode(audio[1], offload_latent_to_cpu=False)  # [2, N] -> [64, T]
     assert z1.shape == (64, T)
+    with pytest.raises(ValueError):                             # vae_encode.py:70-72: stride <= 0
+        h.tiled_encode(audio, chunk_size=n - 1)                 # default overlap 2 s > chunk / 2
     torch.cuda.synchronize()
 
 

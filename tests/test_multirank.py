@@ -81,3 +81,22 @@ def test_bench_under_torchrun():
 def test_bench_refuses_world_mismatch():
     p = _bench(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+PIPE_WORKER = os.path.join(REPO, "tests", "helpers", "pipeline_worker.py")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_song_parallel_pipeline(tmp_path, world):
+    """SongParallelPipeline: rank 0 conditions the batch once, draws the batch
+    noise, scatters per song; every rank runs its songs; latents gathered in batch order —
+    equal to the single-process batch for an int seed (one generator), per-song seeds with
+    cover noise, and acs < 1 with fewer songs than ranks; the serve loop ends on stop()."""
+    rc = D.launch_local([PIPE_WORKER], world, extra_env={"ACEHIP_TEST_OUT": str(tmp_path)}, timeout=180)
+    assert rc == 0
+    recs = {r: json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)}
+    assert recs[0]["ok"] == [True, True, True]
+    # song i on rank i % world: batch sizes 5, 4, 1 split round-robin; idle ranks run nothing
+    for r in range(world):
+        want = [n for n in (len(D.song_assignment(B, r, world)) for B in (5, 4, 1)) if n]
+        assert recs[r]["calls"] == want, (r, recs[r]["calls"], want)

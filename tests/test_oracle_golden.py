@@ -17,13 +17,16 @@ def _cfg(meta):
 
 @pytest.mark.parametrize("name", ["tiny_float32", "tiny_odd_float32", "tiny_bfloat16",
                                   "tiny_odd_bfloat16", "full2_float32", "full2_bfloat16",
-                                  "full2_long_float32", "full2_long_bfloat16"])
+                                  "full2_long_float32", "full2_long_bfloat16",
+                                  "full24_float32", "full24_bfloat16"])
 def test_dit_forward_matches_reference(name):
+    """full24_*: the real 24-layer decoder (configuration_acestep_v15.py:148-260) at
+    T = 500, Lenc = 200 — the size SURVEY §8c calibrated the parity contract on."""
     meta = golden_manifest()["forward"][name]
     cfg = _cfg(meta)
     g = load_golden("dit_fwd_" + name)
     dtype = g["xt"].dtype
-    W = synth_dit_weights(cfg, seed=meta["seed"], mode="parity")
+    W = synth_dit_weights(cfg, seed=meta["seed"], mode="parity", workers=8)
     cs = float(sum(float(v.double().abs().sum()) for v in W.values()))
     assert abs(cs - meta["weights_checksum"]) <= 1e-9 * abs(cs), "synthetic weights drifted"
     W = {k: v.to(dtype) for k, v in W.items()}

@@ -50,7 +50,9 @@ def _hip_vae(cfg, W, dev, max_T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg_name,T", [("tiny", 6), ("full", 8)])
+# tiny T = 7: every stage is C = 128 (the ru8 residual unit) and the last stage's L = 13440 is not a
+# multiple of its 256-row tile, so the last window reaches ~300 rows past L into the back pad
+@pytest.mark.parametrize("cfg_name,T", [("tiny", 6), ("tiny", 7), ("full", 8)])
 def test_vae_decode_parity(gpu_device, cfg_name, T):
     cfg = VAEConfig.tiny() if cfg_name == "tiny" else VAEConfig()
     W = synth_vae_weights(cfg, seed=5, mode="parity", with_encoder=True)

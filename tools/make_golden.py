@@ -86,7 +86,7 @@ def checksum(W) -> float:
 def gen_forward(M, C, name, cfg: DiTConfig, B, T, Lenc, dtype, seed, t_vals, tr_vals):
     rc = ref_config(C, cfg)
     model = M.AceStepDiTModel(rc).eval()
-    W = synth_dit_weights(cfg, seed=seed, mode="parity")
+    W = synth_dit_weights(cfg, seed=seed, mode="parity", workers=8)
     missing, unexpected = model.load_state_dict(W, strict=False)
     assert not unexpected and all("rotary" in k for k in missing), (missing, unexpected)
     model = model.to(dtype)
@@ -382,6 +382,17 @@ def main_only(which):
             tag = str(dt).split(".")[-1]
             manifest["forward"][f"full2_long_{tag}"] = gen_forward(M, C, f"full2_long_{tag}", full2, 2, 641, 48, dt,
                                                                   22, [0.5, 0.5], [0.5, 0.5])
+    if "full24" in which:
+        # the real 24-layer decoder (configuration_acestep_v15.py:148-260; the layer loop
+        # base:1463-1485) at the size SURVEY §8c calibrated its tolerance on: T = 500,
+        # Lenc = 200, one broadcast timestep for both rows (the CFG production layout)
+        full24 = DiTConfig()
+        assert full24.num_hidden_layers == 24
+        C, M = _import_ref("base")
+        for dt in (torch.float32, torch.bfloat16):
+            tag = str(dt).split(".")[-1]
+            manifest["forward"][f"full24_{tag}"] = gen_forward(M, C, f"full24_{tag}", full24, 2, 500, 200, dt,
+                                                              51, [0.6328125, 0.6328125], [0.6328125, 0.6328125])
     if "tokenizer" in which:
         manifest["tokenizer"] = {f"tiny_{str(dt).split('.')[-1]}": gen_tokenizer(f"tiny_{str(dt).split('.')[-1]}", dt, 41)
                                  for dt in (torch.float32, torch.bfloat16)}
