@@ -91,3 +91,61 @@ def encode_sample(W, cfg, wav: Tensor, noise: Optional[Tensor] = None) -> Tensor
         return mean
     std = F.softplus(sc) + 1e-4
     return mean + std * noise
+
+
+# ---------------------------------------------------------------------------------------------
+# bf16-storage variant (test oracle for the HIP path at the reference's GPU precision): every
+# activation is STORED in bf16 between ops — as the reference's bf16 VAE on the GPU stores it —
+# while each conv / Snake / residual computes in fp32 (MIOpen / rocBLAS bf16 convolutions
+# accumulate in fp32 and round once).  Weights are the weight-norm fusion rounded to bf16.
+# Runs as torch on any device (the full-length GPU tests run it on the GPU in fp32 arithmetic).
+def _rb(x: Tensor) -> Tensor:
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def _wb(W: Dict[str, Tensor], name: str) -> Tensor:
+    Wf = {k: v.float() for k, v in W.items() if k.startswith(name + ".")}
+    return _rb(_w(Wf, name))
+
+
+def _bb(W: Dict[str, Tensor], name: str) -> Optional[Tensor]:
+    return _rb(W[name].float()) if name in W else None
+
+
+def _snake_b(W, prefix, x):
+    return _rb(snake(x, W[prefix + ".alpha"].float(), W[prefix + ".beta"].float()))
+
+
+def _res_unit_b(W, p, x, dilation):
+    y = _rb(F.conv1d(_snake_b(W, p + ".snake1", x), _wb(W, p + ".conv1"), _bb(W, p + ".conv1.bias"),
+                     dilation=dilation, padding=3 * dilation))
+    y = _rb(F.conv1d(_snake_b(W, p + ".snake2", y), _wb(W, p + ".conv2"), _bb(W, p + ".conv2.bias")))
+    return _rb(x + y)
+
+
+def decode_bf16_storage(W: Dict[str, Tensor], cfg, z: Tensor) -> Tensor:
+    """``decode`` with bf16 activations between ops and fp32 math inside each (see above)."""
+    x = _rb(F.conv1d(_rb(z.float()), _wb(W, "decoder.conv1"), _bb(W, "decoder.conv1.bias"), padding=3))
+    for j, (_cin, _cout, s) in enumerate(cfg.decoder_block_channels()):
+        p = f"decoder.block.{j}"
+        x = _snake_b(W, p + ".snake1", x)
+        x = _rb(F.conv_transpose1d(x, _wb(W, p + ".conv_t1"), _bb(W, p + ".conv_t1.bias"),
+                                   stride=s, padding=math.ceil(s / 2)))
+        for n, d in ((1, 1), (2, 3), (3, 9)):
+            x = _res_unit_b(W, f"{p}.res_unit{n}", x, d)
+    x = _snake_b(W, "decoder.snake1", x)
+    return F.conv1d(x, _wb(W, "decoder.conv2"), None, padding=3)
+
+
+def encode_mean_bf16_storage(W: Dict[str, Tensor], cfg, wav: Tensor) -> Tensor:
+    """``encode_sample(noise=None)`` (the mean) with bf16 activations between ops."""
+    x = _rb(F.conv1d(_rb(wav.float()), _wb(W, "encoder.conv1"), _bb(W, "encoder.conv1.bias"), padding=3))
+    for j, (_cin, _cout, s) in enumerate(cfg.encoder_block_channels()):
+        p = f"encoder.block.{j}"
+        for n, d in ((1, 1), (2, 3), (3, 9)):
+            x = _res_unit_b(W, f"{p}.res_unit{n}", x, d)
+        x = _snake_b(W, p + ".snake1", x)
+        x = _rb(F.conv1d(x, _wb(W, p + ".conv1"), _bb(W, p + ".conv1.bias"), stride=s, padding=math.ceil(s / 2)))
+    x = _snake_b(W, "encoder.snake1", x)
+    h = F.conv1d(x, _wb(W, "encoder.conv2"), _bb(W, "encoder.conv2.bias"), padding=1)
+    return h.chunk(2, dim=1)[0]
