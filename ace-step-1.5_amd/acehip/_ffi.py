@@ -27,6 +27,7 @@ EXPORTS = [
     "acehip_dit_profile", "acehip_dit_profile_read", "acehip_dit_profile_kinds",
     "acehip_sampler_apg_euler", "acehip_sampler_adg_euler", "acehip_sampler_axpy",
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
+    "acehip_vae_decode_blocks",
     "acehip_vae_encode", "acehip_vae_destroy", "acehip_vae_conv", "acehip_vae_resunit",
     "acehip_wav_peak_normalize", "acehip_wav_postprocess",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
@@ -88,6 +89,7 @@ def _declare(lib):
         "acehip_vae_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
         "acehip_vae_finalize": (c_int, [P]),
         "acehip_vae_decode": (c_int, [P, P, c_int, c_int, P, P]),
+        "acehip_vae_decode_blocks": (c_int, [P, P, c_int, c_int, P, P]),
         "acehip_vae_encode": (c_int, [P, P, c_int, c_int, P, P, P]),
         "acehip_vae_destroy": (c_int, [P]),
         "acehip_vae_conv": (c_int, [c_int, P, c_int64, c_int, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P]),

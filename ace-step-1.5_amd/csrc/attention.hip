@@ -38,6 +38,7 @@
 // attn_pw_kernel (band layers by default, ACEHIP_ATTN_PW): the same math with 64 query
 // rows per wave at one wave per SIMD, O / Q / K in asm-owned AGPRs and the softmax VALU
 // hand-placed between the MFMAs (its header below has the schedule and the A/B numbers).
+#include <atomic>
 #include <type_traits>
 #include "kernels.h"
 
@@ -78,6 +79,15 @@ struct SplitArgs {
     float *ws;     // ≥ (units − full)·nsplit·8·66·64 floats
     int *cnt;      // ≥ units − full ints, zero between launches
     int units = 0; // attn_pw_kernel: > 0 = persistent over units [0, units) (no splits)
+    // attn_fwd_kernel stream-K mode (sk_total > 0): the units' KV tiles form one sequence of
+    // sk_total = units · sk_nt tiles (unit-major); workgroup c runs tiles
+    // [c·total/grid, (c+1)·total/grid) as pieces of at most a few units.  A piece that does not
+    // start at its unit's tile 0 is the first piece of its workgroup: it publishes its partial
+    // (O, m, l) as slab c (write-through stores) and then flags[c] = epoch; the piece holding
+    // tile 0 (its workgroup's LAST piece, so the later pieces were published long before) folds
+    // its own partial with slabs c+1, c+2, … in that order and writes O.
+    int sk_total = 0, sk_nt = 0, epoch = 0;
+    int *flags = nullptr;   // ≥ grid ints; monotonic epochs, never reset
 };
 
 // ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
@@ -253,13 +263,28 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     // XCD-aware: the blocks one XCD receives (bid ≡ x mod 8) take a contiguous unit range,
     // so the q-blocks of one (b, kv head) share that XCD's L2 copy of its K/V tiles
     // (whole units only: the tail-split parts must stay the grid's last blocks)
+    const bool streamk = sp.sk_total > 0;
+    int64_t g0 = 0, g1 = 0;                 // stream-K: this workgroup's global tile range
+    if (streamk) {
+        g0 = (int64_t)blockIdx.x * sp.sk_total / gridDim.x;
+        g1 = ((int64_t)blockIdx.x + 1) * sp.sk_total / gridDim.x;
+        if (g0 >= g1) return;
+    }
+    for (;;) {                              // pieces (one unless stream-K)
     int u = blockIdx.x, part = 0, nsplit = 1;
-    if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
-    if (u >= sp.full) {
-        const int j = u - sp.full;
-        u = sp.full + j / sp.nsplit;
-        part = j % sp.nsplit;
-        nsplit = sp.nsplit;
+    int pt0 = 0, pt1 = 0;                   // stream-K: this piece's tiles [pt0, pt1) of unit u
+    if (streamk) {
+        u = (int)(g0 / sp.sk_nt);
+        pt0 = (int)(g0 % sp.sk_nt);
+        pt1 = (int)min<int64_t>(sp.sk_nt, pt0 + (g1 - g0));
+    } else {
+        if (ATT_XCD && u < sp.full) u = xcd_remap(u, sp.full);
+        if (u >= sp.full) {
+            const int j = u - sp.full;
+            u = sp.full + j / sp.nsplit;
+            part = j % sp.nsplit;
+            nsplit = sp.nsplit;
+        }
     }
     // head group hg of NREP query heads; hpw head groups share one KV head
     const int hpw = H / (KV * NREP);
@@ -302,6 +327,10 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         const int t0 = min(ntiles, part * per), t1 = min(ntiles, t0 + per);
         t_first += t0;
         ntiles = t1 - t0;
+    }
+    if (streamk) {                                 // unmasked full / cross: every unit has sk_nt tiles
+        t_first += pt0;
+        ntiles = pt1 - pt0;
     }
 
     // LDS-DMA staging of one K/V tile (32 KiB = 32 wave-instructions of 1 KiB, 4 per
@@ -579,7 +608,46 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         if (tid == 0) sp.cnt[u - sp.full] = 0;         // self-resetting for the next launch
     }
 
-    if (qi >= Sq) return;                     // both lanes of a row pair (lane, lane ^ 32) leave together
+    bool write_o = true;
+    if (streamk && !(pt0 == 0 && pt1 == sp.sk_nt)) {
+        const int64_t wsz = 66 * 64;                   // floats per wave: 64 O + m + l per lane
+        if (pt0 > 0) {
+            // a later piece of unit u (this workgroup's first piece): publish slab c, then the flag
+            slab_store(sp.ws + ((int64_t)blockIdx.x * 8 + wave) * wsz, oacc, m, l, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(sp.flags + blockIdx.x, sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            write_o = false;
+        } else {
+            // the piece with tile 0 (this workgroup's last): fold the later pieces in order — the
+            // first pieces of workgroups c+1, c+2, … that start inside unit u
+            const int64_t uend = ((int64_t)u + 1) * sp.sk_nt;
+            for (int c2 = blockIdx.x + 1; c2 < (int)gridDim.x; ++c2) {
+                if ((int64_t)c2 * sp.sk_total / gridDim.x >= uend) break;
+                __shared__ int s_ok;
+                if (tid == 0) {
+                    int ok = 0;
+                    for (int spin = 0; spin < (1 << 22); ++spin) {      // bounded: give up, never hang
+                        if (__hip_atomic_load(sp.flags + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sp.epoch) {
+                            ok = 1;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    s_ok = ok;
+                }
+                __syncthreads();
+                f32x16 o2[4];
+                float m2, l2;
+                slab_load(sp.ws + ((int64_t)c2 * 8 + wave) * wsz, o2, m2, l2, lane);
+                if (!s_ok) m2 = __builtin_nanf("");      // timed out: poison the row rather than hang
+                slab_fold(oacc, m, l, o2, m2, l2, false);
+                __syncthreads();
+            }
+        }
+    }
+
+    if (write_o && qi < Sq) {                 // both lanes of a row pair (lane, lane ^ 32) agree
     const float inv = 1.0f / l;
     bf16_t *op = o + ((int64_t)b * Sq + qi) * o_ld + hq * 128;
     // lane (r, hh) holds columns 32dt + 8gg + 4hh .. +3 of its row; the two half-waves swap one
@@ -599,6 +667,11 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
             }
             *(uint4 *)(op + 32 * dt + 16 * gp + 8 * hh) = pack8(v);
         }
+    }
+    if (!streamk) break;
+    g0 += ntiles;
+    if (g0 >= g1) break;
+    }   // pieces
 }
 
 // ---------------------------------------------------------------------------
@@ -1284,7 +1357,16 @@ static int short_tpp() { return knobs().attn_short_tpp; }
 
 size_t attention_ws_bytes() {
     const size_t cus = std::max<size_t>(1024, (size_t)num_cus_attn());
-    return cus * 8 * 66 * 64 * sizeof(float) + cus * sizeof(int);   // ≤ cus split parts in flight
+    // [tail-split tickets: cus ints][slabs: cus · 8 waves · 66·64 floats][stream-K flags: cus ints]
+    return cus * 8 * 66 * 64 * sizeof(float) + 2 * cus * sizeof(int);   // ≤ cus split parts in flight
+}
+
+// stream-K epochs: one per launch, process-wide, so a flag word never holds a value a later
+// launch could mistake for its own (the workspace is zeroed once at allocation)
+static int next_epoch() {
+    static std::atomic<int> e{0};
+    int v = e.fetch_add(1, std::memory_order_relaxed) + 1;
+    return v > 0 ? v : 1;
 }
 
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
@@ -1370,7 +1452,24 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.cnt = (int *)ws;
         sp.ws = (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int));
     }
-    const int grid = sp.full + (units - sp.full) * sp.nsplit;
+    int grid = sp.full + (units - sp.full) * sp.nsplit;
+    // stream-K (ACEHIP_ATTN_STREAMK): unmasked full layers whose units do not divide into whole
+    // rounds run as ONE round of `cus` workgroups over the units' concatenated KV tiles, instead
+    // of a whole round + tail-split parts (a second round's fixed cost).  240 s full attention
+    // (384 units × 47 tiles on 256 CUs) 186.1 → 175.8 µs in one process; the one-round cross grid
+    // (192 units × 11 tiles) loses, 34.8 → 45.8 (its pieces' restart + merge ≥ the 2.75 tiles
+    // saved), so only grids of more units than CUs and long loops take it
+    if (kn.attn_streamk && ws && nrep == 2 && window < 0 && !kmask && units > cus && units % cus != 0 &&
+        unit_tiles >= 24) {
+        const size_t wcus = (size_t)std::max(1024, cus);
+        sp = SplitArgs{nq, units, 1, nullptr, nullptr};
+        sp.sk_nt = unit_tiles;
+        sp.sk_total = units * unit_tiles;
+        sp.epoch = next_epoch();
+        sp.ws = (float *)((char *)ws + wcus * sizeof(int));
+        sp.flags = (int *)((char *)ws + wcus * sizeof(int) + wcus * 8 * 66 * 64 * sizeof(float));
+        grid = cus;
+    }
     if (nrep == 2) {
         attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else if (nrep == 1) {

@@ -21,6 +21,7 @@ struct Knobs {
     int attn_pw_split = 24;   // ACEHIP_ATTN_PW_SPLIT: shortest KV loop whose tail units are split
     int attn_short_tpp = 3;   // ACEHIP_ATTN_SHORT_TPP: KV tiles per part of the short split
     int attn_cus = 0;         // ACEHIP_ATTN_CUS: CU count the splits plan for (0: the device's)
+    int attn_streamk = 1;     // ACEHIP_ATTN_STREAMK: stream-K rounds for unmasked full / cross layers
     int fuse_rowadd = 1;      // ACEHIP_FUSE_ROWADD: null-row constant added in the MLP norm
     int dit_dedup = 1;        // ACEHIP_DIT_DEDUP: layer-0 CFG row dedup
     int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body

@@ -32,6 +32,7 @@ Knobs read_env() {
     k.attn_short_tpp = env_int("ACEHIP_ATTN_SHORT_TPP", 3);
     if (k.attn_short_tpp <= 0) k.attn_short_tpp = 3;
     k.attn_cus = env_int("ACEHIP_ATTN_CUS", 0);
+    k.attn_streamk = env_int("ACEHIP_ATTN_STREAMK", 1);
     k.fuse_rowadd = env_int("ACEHIP_FUSE_ROWADD", 1);
     k.dit_dedup = env_int("ACEHIP_DIT_DEDUP", 1);
     k.dit_graph = env_int("ACEHIP_DIT_GRAPH", 0);

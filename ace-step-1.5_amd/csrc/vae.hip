@@ -398,6 +398,41 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
     return 0;
 }
 
+int acehip_vae_decode_blocks(acehip_vae *h, const void *z, int T, int n_blocks, void *act, void *stream) {
+    if (!h || !z || !act) return fail(ACEHIP_E_ARG, "null argument");
+    if (!h->finalized) return fail(ACEHIP_E_STATE, "vae_decode_blocks before finalize");
+    const int n = h->cfg.n_blocks, Cz = h->cfg.latent_channels;
+    if (T <= 0 || T > h->cfg.max_T || n_blocks < 0 || n_blocks > n)
+        return fail(ACEHIP_E_ARG, "vae_decode_blocks: T or n_blocks out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    // the same launches as acehip_vae_decode, stopped after block n_blocks
+    bf16_t *X = h->X, *cur = h->P, *other = h->Q;
+    if ((rc = cf_to_nlc((const bf16_t *)z, Cz, T, X, s))) return rc;
+    if ((rc = run_conv(h->zero, h->dconv1, X, T, T, 7, 1, 1, -3, 1, 0, T, nullptr, cur, &h->dec[0].snake, nullptr, 1, s)))
+        return rc;
+    int64_t L = T, C = h->dec[0].cin;
+    for (int j = 0; j < n_blocks; ++j) {
+        const auto &bk = h->dec[j];
+        const int st = bk.stride, pad = (st + 1) / 2;
+        if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
+                           nullptr, st, s)))
+            return rc;
+        L *= st;
+        C = bk.cout;
+        std::swap(cur, other);
+        for (int u = 0; u < 3; ++u) {
+            const SnakeP &next = u < 2 ? bk.res[u + 1].s1 : (j + 1 < n ? h->dec[j + 1].snake : h->dsnake);
+            rc = res_unit(h->zero, bk.res[u], L, X, cur, other, next, u < 2, s);
+            if (rc == 1) std::swap(cur, other);
+            else if (rc) return rc;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(act, cur, (size_t)L * C * 2, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
 int acehip_vae_encode(acehip_vae *h, const void *wav, int B, int N, const void *eps, void *z_out, void *stream) {
     if (!h || !wav || !z_out) return fail(ACEHIP_E_ARG, "null argument");
     if (!h->finalized || !h->cfg.with_encoder) return fail(ACEHIP_E_STATE, "vae_encode: encoder not loaded");

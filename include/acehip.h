@@ -290,6 +290,12 @@ int acehip_vae_finalize(acehip_vae *h);
  * z: bf16 [B, 64, T] → wav fp32 [B, 2, T*hop]; untiled (the decoder's
  * receptive field is < the reference's 64-frame overlap). */
 int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, void *stream);
+/* Test entry (block-level parity): the first launches of acehip_vae_decode for ONE song
+ * (z bf16 [1, 64, T]) — conv1 and decoder blocks 0 .. n_blocks-1 — and a copy of the
+ * activation they leave: channels-last bf16 [L][C] (L = T·Π strides so far), already passed
+ * through the NEXT Snake (block n_blocks' snake1, or decoder.snake1 after the last block),
+ * i.e. exactly the input of the next stage (vae_model.py:119-142, 190-230). */
+int acehip_vae_decode_blocks(acehip_vae *h, const void *z, int T, int n_blocks, void *act, void *stream);
 
 /* vae.encode(x).latent_dist.sample() (vae_encode.py:65) — and, untiled, the
  * handler's tiled_encode (vae_encode.py:15-82: the encoder's receptive field is

@@ -907,3 +907,33 @@ def test_cross_kv_grouped_gemms(gpu_device, monkeypatch):
                                      ctx.cpu()).float()
     assert rel_l2(outs[1], outs[0]) < 1e-3, rel_l2(outs[1], outs[0])
     assert rel_l2(outs[1], ref) <= TOL_REL and cosine(outs[1], ref) >= TOL_COS
+
+
+@pytest.mark.parametrize("cus,B,H,KV,Sq,Sk", [(16, 2, 4, 2, 700, 1600), (20, 2, 4, 2, 700, 3100), (0, 2, 16, 8, 3000, 3000),
+                                              (0, 2, 16, 8, 7500, 7500), (7, 1, 4, 2, 1000, 1700), (3, 1, 2, 1, 450, 1600)])
+def test_attention_streamk(gpu_device, monkeypatch, cus, B, H, KV, Sq, Sk):
+    """Stream-K rounds (ACEHIP_ATTN_STREAMK=1) for unmasked full / cross layers: the units' KV tiles
+    as one sequence split evenly over the workgroups; pieces past a unit's tile 0 publish their
+    partial (O, m, l) and the piece holding tile 0 folds them in order.  ACEHIP_ATTN_CUS shrinks the
+    grid so units span 2-3 workgroups; cus = 0 is the real 240 s full / cross shape.  vs fp32, and
+    bit-identical across launches (the epoch flags are never reset)."""
+    if cus:
+        set_knob(monkeypatch, "ACEHIP_ATTN_CUS", str(cus))
+    set_knob(monkeypatch, "ACEHIP_ATTN_STREAMK", "1")
+    set_knob(monkeypatch, "ACEHIP_ATTN_PW", "2")
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(Sq + Sk + cus)
+    q = torch.randn(B, H, Sq, 128, generator=g).to(gpu_device, torch.bfloat16)
+    k = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
+    v = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        o = torch.full((B, Sq, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, Sq, Sk, -1,
+                                                1 / math.sqrt(128), ff.stream_ptr()))
+        torch.cuda.synchronize()
+        outs.append(o)
+    ref = _attn_ref(q, k, v, -1).transpose(1, 2).reshape(B, Sq, H * 128)
+    assert torch.isfinite(outs[0].float()).all()
+    assert rel_l2(outs[0].float().cpu(), ref.float().cpu()) < 1e-2
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
