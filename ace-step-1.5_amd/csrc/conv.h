@@ -38,6 +38,12 @@ struct ResUnitArgs {
     bf16_t *out_s;
     const float *sa_next, *sib_next;
     int keep_raw;
+    // snake_in (ru8_kernel only): c1.in is the RAW x (= x); the unit's first Snake (sa_in / sib_in)
+    // is applied while the window is staged, so no x_s tensor exists; keep_raw then writes x' to
+    // x_out (a different buffer: neighbouring tiles' windows still read x), else out_s as usual
+    int snake_in = 0;
+    const float *sa_in = nullptr, *sib_in = nullptr;
+    bf16_t *x_out = nullptr;
 };
 int resunit128(const ResUnitArgs &u, hipStream_t s);
 // W2 [n_rows][128] → columns permuted within each 32-block so that the k=7 accumulator

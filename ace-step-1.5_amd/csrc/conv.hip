@@ -1089,6 +1089,8 @@ __global__ __launch_bounds__(256, 2) void ru7_kernel(ResUnitArgs u, int64_t ntil
 // before it have landed (vmcnt retires in order), and every chunk a K-tile reads was issued
 // before the W that K-tile's barrier waits for.
 // LDS: 2 560 (parameters) + 2 × 39 680 (windows: 310 rows × 64 channels) + 3 × 16 KiB = 128 KiB.
+template <int V>
+using IC7 = std::integral_constant<int, V>;
 template <int I0, int I1, typename F>
 __device__ __forceinline__ void sfor(F &&f) {     // compile-time unrolled loop (f gets an integral_constant)
     if constexpr (I0 < I1) {
@@ -1146,6 +1148,18 @@ __host__ __device__ constexpr int allowed(int kt, int h, bool first, bool more) 
         n += s >= 0 ? step_count(s, h, first, more) : step_count(s + 16, h, false, true);
     return n;
 }
+// snake_in (SIN) variant: one wave issues every W piece (16 per K-tile), so before barrier kt
+// the W pieces newer than W(kt) are those of K-tiles kt+1 .. kt+D−1 already issued
+__host__ __device__ constexpr int w_newer(int kt, bool more) {
+    int n = 0;
+    for (int j = kt + 1; j < kt + D; ++j)
+        if (j <= 15 || more) n += 16;
+    return n;
+}
+// window pieces per step in the SIN variant (loads issued in step s, snaked and written to LDS in
+// step s + 1): chunk 1 of the current tile (steps 0-3, not the block's first tile), chunk 0 of
+// the next tile (steps 7-12), the first part of its chunk 1 (steps 14-15) — the same ranges as
+// the DMA schedule above
 }  // namespace ru8
 
 // vmcnt(N) with N a template constant (N ≤ 63)
@@ -1186,8 +1200,49 @@ __device__ __forceinline__ void ru8_w(const ResUnitArgs &u, uint32_t slot, int k
     }
 }
 
-template <bool RAW>
-__global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
+// timing experiments only (wrong results): epilogue 2 without the next Snake / without the
+// snaked store when the raw one is kept
+#ifndef RU8_X_NOSNAKE2
+#define RU8_X_NOSNAKE2 0
+#endif
+#ifndef RU8_X_NOSTORE_S
+#define RU8_X_NOSTORE_S 0
+#endif
+// SIN window helper H (H = 0 / 1: pieces q ≡ H mod 2): global 16-B loads of raw x into registers,
+// Snake (the unit's first, sa_in / sib_in), bf16, LDS — the same image the LDS-DMA would write
+// from x_s.  Plain loads: hipcc counts them and waits for the data of step s only where step
+// s + 1 writes it out (inline-asm loads would leave a register copy of an unlanded destination
+// possible between the load and its wait).
+template <int H, int P0, int P1>
+__device__ __forceinline__ void sin_issue(const char *src, uint32_t goff, int l3, uint4 (&ld)[4]) {
+    int k = 0;
+#pragma unroll
+    for (int q = P0; q < P1; ++q) {
+        if ((q & 1) != H) continue;
+        if (q * 8 + 8 <= ru8::WROWS || l3 < ru8::WROWS - q * 8) ld[k] = *(const uint4 *)(src + (int64_t)q * 8 * 256 + goff);
+        ++k;
+    }
+}
+template <int H, int P0, int P1>
+__device__ __forceinline__ void sin_write(char *buf, uint32_t loff, int l3, const uint4 (&ld)[4], const float (&sa)[8],
+                                          const float (&sb)[8]) {
+    int k = 0;
+#pragma unroll
+    for (int q = P0; q < P1; ++q) {
+        if ((q & 1) != H) continue;
+        if (q * 8 + 8 <= ru8::WROWS || l3 < ru8::WROWS - q * 8) {
+            float x[8], y[8];
+            unpack8(ld[k], x);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = snake1(x[e], sa[e], sb[e]);
+            *(uint4 *)(buf + q * 1024 + loff) = pack8(y);
+        }
+        ++k;
+    }
+}
+
+template <bool RAW, bool SIN = false>
+__global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
     constexpr int RBM = ru8::BM, WINB = ru8::WINB, WT = ru8::WT;
     __shared__ __attribute__((aligned(16))) char lds[ru8::LDS];
     const ConvArgs &a = u.c1;
@@ -1201,7 +1256,109 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
     float *psa2 = (float *)par, *psib2 = psa2 + 128, *psan = psa2 + 256, *psibn = psa2 + 384;
     bf16_t *pb1 = (bf16_t *)(par + 2048), *pb2 = (bf16_t *)(par + 2304);
 
-    if (wave >= 4) {
+    if (SIN && wave == 4) {
+        // ---- SIN: one helper wave issues every W piece ----
+        const int l3 = lane >> 3, lc = ((lane & 7) ^ l3) * 16;
+        const uint32_t vk1 = l3 * 1792 + lc, vk2 = l3 * 256 + lc;
+#pragma unroll
+        for (int k = 0; k < ru8::D; ++k) {
+            ru8_w(u, wr3 + k * WT, k, 0, vk1, vk2);
+            ru8_w(u, wr3 + k * WT, k, 1, vk1, vk2);
+        }
+        int slot = 0;
+        for (int64_t t = t0; t < t1; ++t) {
+            const bool more = t + 1 < t1;
+            sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
+                constexpr int kt = decltype(KT)::value;
+                if (more) vm_wait<ru8::w_newer(kt, true)>();
+                else vm_wait<ru8::w_newer(kt, false)>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                const int sp = slot == 0 ? ru8::NSLOT - 1 : slot - 1;
+                if constexpr (kt + ru8::D <= 15) {
+                    ru8_w(u, wr3 + sp * WT, kt + ru8::D, 0, vk1, vk2);
+                    ru8_w(u, wr3 + sp * WT, kt + ru8::D, 1, vk1, vk2);
+                } else if (more) {
+                    ru8_w(u, wr3 + sp * WT, kt + ru8::D - 16, 0, vk1, vk2);
+                    ru8_w(u, wr3 + sp * WT, kt + ru8::D - 16, 1, vk1, vk2);
+                }
+                slot = slot + 1 == ru8::NSLOT ? 0 : slot + 1;
+            });
+        }
+        vm_wait<0>();
+        return;
+    }
+    if (SIN && wave >= 5) {
+        // ---- SIN: two window helpers (raw x → Snake → LDS) ----
+        auto run = [&](auto HC) __attribute__((always_inline)) {
+            constexpr int H = decltype(HC)::value;
+            const int l3 = lane >> 3, c = (lane & 7) ^ l3;
+            const uint32_t goff = l3 * 256 + c * 16, loff = lane * 16;
+            float sa[2][8], sb[2][8];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    sa[cc][e] = u.sa_in[cc * 64 + c * 8 + e];
+                    sb[cc][e] = u.sib_in[cc * 64 + c * 8 + e];
+                }
+            int dl = a.dil;
+            asm volatile("" : "+s"(dl));
+            auto src_of = [&](int64_t m0, int cc) __attribute__((always_inline)) {
+                return (const char *)(a.in + (m0 - 3 * dl) * 128) + cc * 128;
+            };
+            uint4 ld[2][4];
+            // prologue: the block's first tile, both chunks, in batches of ≤ 4 pieces
+            {
+                const int64_t m0 = t0 * RBM;
+                sfor<0, 2>([&](auto CCC) __attribute__((always_inline)) {
+                    constexpr int cc = decltype(CCC)::value;
+                    sfor<0, 5>([&](auto BC) __attribute__((always_inline)) {
+                        constexpr int p0 = decltype(BC)::value * 8, p1 = p0 + 8 < ru8::NPW ? p0 + 8 : ru8::NPW;
+                        sin_issue<H, p0, p1>(src_of(m0, cc), goff, l3, ld[0]);
+                        sin_write<H, p0, p1>(win + cc * WINB, loff, l3, ld[0], sa[cc], sb[cc]);
+                    });
+                });
+            }
+            for (int64_t t = t0; t < t1; ++t) {
+                const int64_t m0 = t * RBM;
+                const bool first = t == t0, more = t + 1 < t1;
+                sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
+                    constexpr int kt = decltype(KT)::value, PB = kt & 1, PP = PB ^ 1;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's LDS writes landed
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" ::: "memory");
+                    // issue step kt's loads into ld[PB] (the ranges of the DMA schedule)
+                    if constexpr (kt <= 3) {
+                        if (!first) sin_issue<H, ru8::c1b_lo(kt), ru8::c1b_hi(kt)>(src_of(m0, 1), goff, l3, ld[PB]);
+                    } else if constexpr (kt >= 7 && kt <= 12) {
+                        if (more) sin_issue<H, ru8::c0_lo(kt - 7), ru8::c0_hi(kt - 7)>(src_of(m0 + RBM, 0), goff, l3, ld[PB]);
+                    } else if constexpr (kt >= 14) {
+                        if (more) sin_issue<H, ru8::c1a_lo(kt - 14), ru8::c1a_hi(kt - 14)>(src_of(m0 + RBM, 1), goff, l3, ld[PB]);
+                    }
+                    // finish step kt − 1's pieces (loaded into ld[PP]): Snake, LDS
+                    auto fin = [&](auto P0C, auto P1C, auto CCC) __attribute__((always_inline)) {
+                        constexpr int p0 = decltype(P0C)::value, p1 = decltype(P1C)::value, cc = decltype(CCC)::value;
+                        sin_write<H, p0, p1>(win + cc * WINB, loff, l3, ld[PP], sa[cc], sb[cc]);
+                    };
+                    if constexpr (kt >= 1 && kt <= 4) {          // chunk 1 of this tile, issued at kt − 1
+                        if (!first) fin(IC7<ru8::c1b_lo(kt - 1)>{}, IC7<ru8::c1b_hi(kt - 1)>{}, IC7<1>{});
+                    } else if constexpr (kt >= 8 && kt <= 13) {  // chunk 0 of the next tile
+                        if (more) fin(IC7<ru8::c0_lo(kt - 8)>{}, IC7<ru8::c0_hi(kt - 8)>{}, IC7<0>{});
+                    } else if constexpr (kt == 15) {             // chunk 1 (first part) of the next tile
+                        if (more) fin(IC7<ru8::c1a_lo(0)>{}, IC7<ru8::c1a_hi(0)>{}, IC7<1>{});
+                    } else if constexpr (kt == 0) {              // issued at step 15 of the previous tile
+                        if (!first) fin(IC7<ru8::c1a_lo(1)>{}, IC7<ru8::c1a_hi(1)>{}, IC7<1>{});
+                    }
+                });
+            }
+            vm_wait<0>();
+        };
+        if (wave == 5) run(IC7<0>{});
+        else run(IC7<1>{});
+        return;
+    }
+    if (!SIN && wave >= 4) {
         // ---- helper waves: every LDS-DMA of the block ----
         const int h = wave - 4;
         const int l3 = lane >> 3, lc = ((lane & 7) ^ l3) * 16;
@@ -1402,12 +1559,19 @@ __global__ __launch_bounds__(384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntil
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
-                    sn[r] = snake1(o[r], av[r], sv[r]);
+                    if constexpr (!(SIN && RAW)) sn[r] = RU8_X_NOSNAKE2 ? o[r] : snake1(o[r], av[r], sv[r]);
                 }
                 const int64_t m = me + 64 * wave + 16 * i + fr;
                 if (m < a.M) {
-                    if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
-                    *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+                    if constexpr (SIN) {
+                        // raw x' for the next unit (which snakes it while staging), or the
+                        // block's snaked output
+                        if constexpr (RAW) *(uint4 *)(u.x_out + m * 128 + n) = pack8(o);
+                        else *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+                    } else {
+                        if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
+                        if (!(RAW && RU8_X_NOSTORE_S)) *(uint4 *)(u.out_s + m * 128 + n) = pack8(sn);
+                    }
                 }
             }
         }
@@ -1700,12 +1864,22 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
     const ConvArgs &a = u.c1;
     if (a.Cin != 128 || a.N != 128 || a.taps != 7 || !a.zero || !a.bias || !a.sa) return fail(-1, "resunit128: args");
     if (u.x == u.out_s || a.in == u.out_s) return fail(-1, "resunit128: out_s must not alias x / x_s");
+    if (u.snake_in && !(knobs().ru7 == 2 && u.W2p && u.in_zero_pad && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M))
+        return fail(-1, "resunit128: snake_in runs on ru8_kernel only");
     if (knobs().ru7 == 2 && u.W2p && u.in_zero_pad && a.dil <= 9 && a.a_off == -3 * a.dil && a.L_in == a.M) {
         const int64_t nt = (a.M + ru8::BM - 1) / ru8::BM;
         const int nb = (int)std::min<int64_t>(nt, (int64_t)num_cus_conv());
         HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * 128), 0, (size_t)kActPadRows * 256, s));
-        if (u.keep_raw) ru8_kernel<true><<<nb, 384, 0, s>>>(u, nt);
-        else ru8_kernel<false><<<nb, 384, 0, s>>>(u, nt);
+        if (u.snake_in) {
+            if (!u.sa_in || !u.sib_in || (u.keep_raw && (!u.x_out || u.x_out == u.x)) || a.in != u.x)
+                return fail(-1, "resunit128: snake_in needs sa_in / sib_in, in == x and a separate x_out");
+            if (u.keep_raw) ru8_kernel<true, true><<<nb, 448, 0, s>>>(u, nt);
+            else ru8_kernel<false, true><<<nb, 448, 0, s>>>(u, nt);
+        } else if (u.keep_raw) {
+            ru8_kernel<true><<<nb, 384, 0, s>>>(u, nt);
+        } else {
+            ru8_kernel<false><<<nb, 384, 0, s>>>(u, nt);
+        }
         HIP_TRY(hipGetLastError());
         return 0;
     }

@@ -28,6 +28,7 @@ struct Knobs {
     int conv7 = 1;            // ACEHIP_CONV7: halo-staged k = 7 VAE convs
     int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
     int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
+    int vae_snake_in = 1;     // ACEHIP_VAE_SNAKE_IN: C = 128 decoder blocks without x_s tensors (ru8 SIN)
     int kv_group_kib = 262144; // ACEHIP_KV_GROUP_KIB: cross-K/V scratch bound at dit_create (tests force small groups)
     unsigned gen = 0;
 };

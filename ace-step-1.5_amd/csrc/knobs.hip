@@ -40,6 +40,7 @@ Knobs read_env() {
     k.convp = env_int("ACEHIP_CONVP", 2);
     k.ru7 = env_int("ACEHIP_RU7", 2);
     k.kv_group_kib = env_int("ACEHIP_KV_GROUP_KIB", 262144);
+    k.vae_snake_in = env_int("ACEHIP_VAE_SNAKE_IN", 1);
     if (k.kv_group_kib <= 0) k.kv_group_kib = 262144;
     return k;
 }

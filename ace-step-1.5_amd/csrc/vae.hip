@@ -189,6 +189,51 @@ int res_unit(const bf16_t *zero, const ResU &r, int64_t L, bf16_t *X, bf16_t *cu
     return run_conv(zero, r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
 }
 
+// ACEHIP_VAE_SNAKE_IN: the C = 128 residual units of a decoder block take RAW x and apply their
+// first Snake while staging the window (ru8_kernel<·, SIN>), so the block's x_s tensors are
+// never written or read (ConvTranspose writes raw x only, units 1-2 write raw x' only)
+bool snake_in_block(const DecBlk &bk) {
+    return knobs().vae_snake_in && knobs().ru7 == 2 && bk.cout == 128 && bk.res[0].W2p && bk.res[1].W2p &&
+           bk.res[2].W2p;
+}
+
+// decoder block j on the snake-in path: in = the block input (snaked), X / cur / other the three
+// buffers (cur = in); returns with the snaked block output in `cur` and X / other free
+int dec_block_snake_in(acehip_vae *h, int j, int64_t &L, bf16_t *&X, bf16_t *&cur, bf16_t *&other, hipStream_t s) {
+    const auto &bk = h->dec[j];
+    const int n = h->cfg.n_blocks, st = bk.stride, pad = (st + 1) / 2;
+    int rc;
+    // ConvTranspose1d → raw x only
+    if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, nullptr, nullptr, nullptr,
+                       st, s)))
+        return rc;
+    L *= st;
+    bf16_t *bufs[3] = {X, cur, other};          // raw x in bufs[0]; unit u: in bufs[u] → out bufs[u + 1 mod 3]
+    for (int u = 0; u < 3; ++u) {
+        const ResU &r = bk.res[u];
+        const SnakeP &next = j + 1 < n ? h->dec[j + 1].snake : h->dsnake;
+        bf16_t *in = bufs[u], *out = bufs[(u + 1) % 3];
+        ResUnitArgs ua{};
+        ConvArgs &a = ua.c1;
+        a.in = in; a.L_in = L; a.Cin = 128; a.W = r.c1.Wp; a.bias = r.c1.bias;
+        a.sa = r.s2.a; a.sib = r.s2.ib; a.L_out = L; a.N = 128; a.M = L;
+        a.taps = 7; a.dil = r.dil; a.a_stride = 1; a.a_off = -3 * r.dil; a.c_stride = 1; a.c_off = 0;
+        a.zero = h->zero;
+        ua.W2 = r.c2.Wp; ua.W2p = r.W2p; ua.b2 = r.c2.bias; ua.x = in;
+        ua.in_zero_pad = 1;
+        ua.snake_in = 1; ua.sa_in = r.s1.a; ua.sib_in = r.s1.ib;
+        ua.keep_raw = u < 2 ? 1 : 0;
+        if (u < 2) ua.x_out = out;
+        else { ua.out_s = out; ua.sa_next = next.a; ua.sib_next = next.ib; }
+        if ((rc = resunit128(ua, s))) return rc;
+    }
+    // the snaked output is in bufs[0] (unit 2: bufs[2] → bufs[0])
+    cur = bufs[0];
+    X = bufs[1];
+    other = bufs[2];
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -380,6 +425,10 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
         for (int j = 0; j < n; ++j) {
             const auto &bk = h->dec[j];
             const int st = bk.stride, pad = (st + 1) / 2;
+            if (snake_in_block(bk)) {
+                if ((rc = dec_block_snake_in(h, j, L, X, cur, other, s))) return rc;
+                continue;
+            }
             // ConvTranspose1d as `st` phase GEMMs → raw x (residual) + snaked x for res_unit1
             if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
                                nullptr, st, s)))
@@ -416,6 +465,11 @@ int acehip_vae_decode_blocks(acehip_vae *h, const void *z, int T, int n_blocks, 
     for (int j = 0; j < n_blocks; ++j) {
         const auto &bk = h->dec[j];
         const int st = bk.stride, pad = (st + 1) / 2;
+        if (snake_in_block(bk)) {
+            if ((rc = dec_block_snake_in(h, j, L, X, cur, other, s))) return rc;
+            C = bk.cout;
+            continue;
+        }
         if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
                            nullptr, st, s)))
             return rc;

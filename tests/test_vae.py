@@ -269,3 +269,28 @@ def test_vae_decode_stagewise_parity(gpu_device, T):
     print(f"VAE stagewise T={T}: " + " ".join(f"{e:.2e}" for e in errs))
     assert all(e <= VAE_STAGE_TOL for e in errs), errs
     be.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name,T", [("tiny", 7), ("full", 150), ("full", 6000)])
+def test_vae_snake_in_blocks(gpu_device, monkeypatch, cfg_name, T):
+    """C = 128 decoder blocks on the snake-in path (ACEHIP_VAE_SNAKE_IN=1, default): the residual
+    units stage raw x and apply their first Snake while staging (no x_s tensors; ConvT writes raw
+    x only, units 1-2 raw x' only, to a second buffer) — the same values as the x_s path
+    (ACEHIP_VAE_SNAKE_IN=0), which computes the same Snake in the producer's epilogue."""
+    from conftest import set_knob
+    cfg = VAEConfig.tiny() if cfg_name == "tiny" else VAEConfig()
+    W = synth_vae_weights(cfg, seed=9, mode="parity", with_encoder=False)
+    be = _hip_vae(cfg, W, gpu_device, max_T=T, with_encoder=False)
+    z = torch.randn(1, 64, T, generator=torch.Generator().manual_seed(T + 3)).bfloat16().to(gpu_device)
+    outs = {}
+    for v in ("0", "1"):
+        set_knob(monkeypatch, "ACEHIP_VAE_SNAKE_IN", v)
+        outs[v] = be.decode(z).sample.clone()
+        torch.cuda.synchronize()
+    be.close()
+    a, b = outs["0"].float().cpu(), outs["1"].float().cpu()
+    assert torch.isfinite(b).all()
+    d = (a - b).abs().max().item()
+    print(f"snake-in vs x_s path {cfg_name} T={T}: max |diff| {d:.3e}, rel-L2 {rel_l2(b, a):.3e}")
+    assert rel_l2(b, a) < 1e-3, (d, rel_l2(b, a))
