@@ -1419,7 +1419,9 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
     // ---- MFMA waves 0-3: rows 64·wave .. +63 of each tile ----
     if (tid < 128) {
         psa2[tid] = a.sa[tid]; psib2[tid] = a.sib[tid];
-        psan[tid] = u.sa_next[tid]; psibn[tid] = u.sib_next[tid];
+        if constexpr (!(SIN && RAW)) {       // the next Snake: only where out_s is written
+            psan[tid] = u.sa_next[tid]; psibn[tid] = u.sib_next[tid];
+        }
         pb1[tid] = a.bias[tid]; pb2[tid] = u.b2[tid];
     }
     const int fr = lane & 15, fc = lane >> 4;
@@ -1870,6 +1872,9 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
         const int64_t nt = (a.M + ru8::BM - 1) / ru8::BM;
         const int nb = (int)std::min<int64_t>(nt, (int64_t)num_cus_conv());
         HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * 128), 0, (size_t)kActPadRows * 256, s));
+        if (!u.snake_in || !u.keep_raw) {
+            if (!u.out_s || !u.sa_next || !u.sib_next) return fail(-1, "resunit128: out_s and the next Snake's parameters");
+        }
         if (u.snake_in) {
             if (!u.sa_in || !u.sib_in || (u.keep_raw && (!u.x_out || u.x_out == u.x)) || a.in != u.x)
                 return fail(-1, "resunit128: snake_in needs sa_in / sib_in, in == x and a separate x_out");

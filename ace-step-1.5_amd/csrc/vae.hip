@@ -223,8 +223,9 @@ int dec_block_snake_in(acehip_vae *h, int j, int64_t &L, bf16_t *&X, bf16_t *&cu
         ua.in_zero_pad = 1;
         ua.snake_in = 1; ua.sa_in = r.s1.a; ua.sib_in = r.s1.ib;
         ua.keep_raw = u < 2 ? 1 : 0;
+        ua.sa_next = next.a; ua.sib_next = next.ib;     // read only by the last unit (out_s)
         if (u < 2) ua.x_out = out;
-        else { ua.out_s = out; ua.sa_next = next.a; ua.sib_next = next.ib; }
+        else ua.out_s = out;
         if ((rc = resunit128(ua, s))) return rc;
     }
     // the snaked output is in bufs[0] (unit 2: bufs[2] → bufs[0])
