@@ -11,6 +11,8 @@
 #   stats[=bench.py args]      rocprofv3 --kernel-trace --stats of a bench run → gpurun_out/<TAG>_stats/
 #   pmc=COUNTERS[=bench args]  one rocprofv3 --pmc pass (counters space-separated) → gpurun_out/<TAG>_pmc_N/
 #   py=SCRIPT[=args]           python -u SCRIPT args (A/B tools, micro-benchmarks)
+#   pystats=SCRIPT[=args]      rocprofv3 --kernel-trace --stats of a python script → gpurun_out/<TAG>_pystats_N/
+#   pypmc=COUNTERS=SCRIPT[=args]  one --pmc pass over a python script → gpurun_out/<TAG>_pypmc_N/
 #   env=VAR=VAL                export VAR=VAL for the following steps
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -54,6 +56,19 @@ for step in "$@"; do
             script=${arg%%=*}; pargs=""
             [ "$script" != "$arg" ] && pargs=${arg#*=}
             run "$(basename "$script" .py)" 900 python -u "$script" $pargs ;;
+        pystats)
+            script=${arg%%=*}; pargs=""
+            [ "$script" != "$arg" ] && pargs=${arg#*=}
+            n_pmc=$((n_pmc + 1))
+            run pystats_$n_pmc 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_pystats_$n_pmc -o run -- \
+                python3 "$script" $pargs ;;
+        pypmc)
+            counters=${arg%%=*}; rest=${arg#*=}
+            script=${rest%%=*}; pargs=""
+            [ "$script" != "$rest" ] && pargs=${rest#*=}
+            n_pmc=$((n_pmc + 1))
+            run pypmc_$n_pmc 240 rocprofv3 --pmc $counters --kernel-trace -d gpurun_out/${TAG}_pypmc_$n_pmc -o run -- \
+                python3 "$script" $pargs ;;
         env)
             export "$arg"; echo "== env $arg" ;;
         *)

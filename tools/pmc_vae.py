@@ -42,7 +42,10 @@ def per_family(db, counter):
     return tot, {k: len(v) for k, v in n.items()}
 
 
-def algorithmic(T):
+def algorithmic(T, snake_in=True):
+    """snake_in (ACEHIP_VAE_SNAKE_IN=1, the default since round 5): the C = 128 blocks keep no x_s
+    tensor — their ConvTranspose writes raw x only and each residual unit reads x once and writes
+    one output (raw x' for units 0, 1; the next block's snaked input for unit 2)."""
     c = VAEConfig()
     B = 2                                                 # bf16 bytes
     fam = defaultdict(float)
@@ -52,11 +55,14 @@ def algorithmic(T):
     L = T
     for cin, cout, s in blocks:
         Lo = L * s
-        fam["conv_gemm_kernel"] += L * cin * B + 2 * Lo * cout * B + cin * cout * 2 * s * B
+        sin = snake_in and cout == 128
+        fam["conv_gemm_kernel"] += L * cin * B + (1 if sin else 2) * Lo * cout * B + cin * cout * 2 * s * B
         L = Lo
         for u in range(3):
             keep = u < 2
-            if cout == 128:
+            if cout == 128 and sin:
+                fam["ru8_kernel"] += 2 * L * cout * B + 8 * cout * cout * B
+            elif cout == 128:
                 fam["ru8_kernel"] += (2 + (2 if keep else 1)) * L * cout * B + 8 * cout * cout * B
             else:
                 fam["conv7_kernel"] += 2 * L * cout * B + 7 * cout * cout * B
@@ -71,10 +77,11 @@ def main():
     p.add_argument("write_db")
     p.add_argument("out_json")
     p.add_argument("--T", type=int, default=6000)
+    p.add_argument("--no-snake-in", action="store_true", help="model of ACEHIP_VAE_SNAKE_IN=0")
     a = p.parse_args()
     F, nF = per_family(a.fetch_db, "FETCH_SIZE")
     W, nW = per_family(a.write_db, "WRITE_SIZE")
-    alg = algorithmic(a.T)
+    alg = algorithmic(a.T, snake_in=not a.no_snake_in)
     out = {"T": a.T, "note": __doc__.split("\n\n")[0], "families": {}}
     tot_m = tot_a = 0.0
     for f in sorted(alg):
