@@ -28,6 +28,11 @@ run() {  # name seconds cmd...
     tail -5 "$log"
     if [ $rc -ne 0 ]; then echo "== $name failed rc=$rc (see $log)"; exit $rc; fi
 }
+summarize() {  # trace dir → markdown kernel table; the trace database itself is dropped (gpurun_out ≤ 64 MiB)
+    local db
+    db=$(find "$1" -name "*.db" | head -1)
+    [ -n "$db" ] && python3 tools/rocprof_summary.py "$db" > "$2" && rm -rf "$1"
+}
 for step in "$@"; do
     kind=${step%%=*}; arg=""
     [ "$kind" != "$step" ] && arg=${step#*=}
@@ -45,7 +50,8 @@ for step in "$@"; do
             grep '^{' gpurun_out/${TAG}_bench.log | tail -1 > gpurun_out/${TAG}_bench.json ;;
         stats)
             run stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_stats -o run -- \
-                python3 bench.py ${arg:---steps 1 --warmup 1 --no-cpu-baseline} ;;
+                python3 bench.py ${arg:---steps 1 --warmup 1 --no-cpu-baseline}
+            summarize gpurun_out/${TAG}_stats gpurun_out/${TAG}_kernel_stats.md ;;
         pmc)
             counters=${arg%%=*}; bargs=""
             [ "$counters" != "$arg" ] && bargs=${arg#*=}
@@ -61,7 +67,8 @@ for step in "$@"; do
             [ "$script" != "$arg" ] && pargs=${arg#*=}
             n_pmc=$((n_pmc + 1))
             run pystats_$n_pmc 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_pystats_$n_pmc -o run -- \
-                python3 "$script" $pargs ;;
+                python3 "$script" $pargs
+            summarize gpurun_out/${TAG}_pystats_$n_pmc gpurun_out/${TAG}_pystats_${n_pmc}_kernel_stats.md ;;
         pypmc)
             counters=${arg%%=*}; rest=${arg#*=}
             script=${rest%%=*}; pargs=""
