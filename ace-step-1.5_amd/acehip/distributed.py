@@ -339,7 +339,13 @@ class SongParallelPipeline:
             e_vae.record()
             self.last_events = (e_dit, e_vae)
         all_lat = sp.gather(lat)
-        all_wav = sp.gather(wav) if (self.gather_wav and wav is not None) else wav
+        all_wav = wav
+        if self.gather_wav and self.vae is not None:
+            if wav is None:           # a rank without songs still joins the collective
+                c = self.vae.cfg
+                wav = torch.zeros(0, c.audio_channels, lat.shape[1] * c.hop_length, device=lat.device,
+                                  dtype=torch.float32)
+            all_wav = sp.gather(wav)
         if sp.rank == 0:
             return {"target_latents": all_lat, "time_costs": costs, "songs": songs, "wav": all_wav}
         return True

@@ -4,7 +4,8 @@ gloo).  The DiT backend is a CPU stand-in with the same surface as AceStepDiTBac
 ``_non_cover`` / ``src_latents``): its "latents" are a fixed function of each song's own
 encoder states, context, noise and sampler arguments, so a song computed on any rank must
 equal the same song computed in the whole batch at once.  Rank 0 sends three requests (int
-seed, seed list + cover noise, acs < 1 with B < world) and one stop; it checks every result
+seed, seed list + cover noise, acs < 1 with B < world) and a stop, then two requests through a
+pipeline with a stand-in VAE and gather_wav (B = 1 < world, B = 5); it checks every result
 against the single-process batch computation and writes $ACEHIP_TEST_OUT/rank<r>.json."""
 import json
 import os
@@ -53,6 +54,21 @@ class StubBackend:
         return {"target_latents": out, "time_costs": {"total_time_cost": 0.0}}
 
 
+class StubVAE:
+    """decode_tensor(z [c, C, T]) → [c, 2, T·hop] fp32, a fixed function of z (CPU)."""
+
+    class cfg:
+        audio_channels, hop_length = 2, 3
+
+    def decode_tensor(self, z):
+        c, C, T = z.shape
+        a = z.float().sum(1, keepdim=True)                            # [c, 1, T]
+        return torch.cat([a, 2 * a], 1).repeat_interleave(3, dim=2)   # [c, 2, 3T]
+
+    def postprocess_(self, wav, normalization_db=None):
+        return wav
+
+
 def request(B, seed, g, **extra):
     kw = dict(text_hidden_states=torch.randn(B, LENC + 2, D_MODEL, generator=g),
               src_latents=torch.randn(B, T, 4, generator=g), chunk_masks=torch.ones(B, T, 4),
@@ -95,9 +111,20 @@ def main():
             else:
                 ok.append(bool(torch.equal(res["target_latents"], ref)))
         pipe.stop()
+        # with a VAE and gather_wav: audio gathered in batch order, also when B < world (ranks
+        # without songs still join the gather)
+        pipe2 = D.SongParallelPipeline(be, StubVAE(), gather_wav=True, normalization_db=None)
+        for B in (1, 5):
+            kw = request(B, 77 + B, g)
+            res = pipe2.generate(**kw)
+            ref = batch_reference(kw)["target_latents"]
+            want = StubVAE().decode_tensor(ref.transpose(1, 2))
+            ok.append(bool(torch.equal(res["wav"], want)) and tuple(res["wav"].shape) == (B, 2, 3 * T))
+        pipe2.stop()
         rec["ok"] = ok
     else:
         pipe.serve()
+        D.SongParallelPipeline(be, StubVAE(), gather_wav=True, normalization_db=None).serve()
     rec["calls"] = be.calls
     D.barrier()
     with open(os.path.join(os.environ["ACEHIP_TEST_OUT"], f"rank{rank}.json"), "w") as f:

@@ -95,8 +95,9 @@ def test_song_parallel_pipeline(tmp_path, world):
     rc = D.launch_local([PIPE_WORKER], world, extra_env={"ACEHIP_TEST_OUT": str(tmp_path)}, timeout=180)
     assert rc == 0
     recs = {r: json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)}
-    assert recs[0]["ok"] == [True, True, True]
-    # song i on rank i % world: batch sizes 5, 4, 1 split round-robin; idle ranks run nothing
+    assert recs[0]["ok"] == [True, True, True, True, True]
+    # song i on rank i % world: batch sizes 5, 4, 1 (then 1, 5 with the VAE) split round-robin;
+    # idle ranks run nothing
     for r in range(world):
-        want = [n for n in (len(D.song_assignment(B, r, world)) for B in (5, 4, 1)) if n]
+        want = [n for n in (len(D.song_assignment(B, r, world)) for B in (5, 4, 1, 1, 5)) if n]
         assert recs[r]["calls"] == want, (r, recs[r]["calls"], want)
