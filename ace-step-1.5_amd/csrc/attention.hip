@@ -712,6 +712,9 @@ constexpr int PW_O = 0, PW_Q = 128, PW_K = 192;
 #ifndef PW_X_NOKREAD
 #define PW_X_NOKREAD 0
 #endif
+#ifndef PW_X_NOMASK
+#define PW_X_NOMASK 0      // band tiles that straddle the band edge processed unmasked
+#endif
 
 __device__ __forceinline__ s16x4 opaque_s16x4() {
     s16x4 r;
@@ -1074,7 +1077,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
             constexpr int sb = decltype(SBC)::value, t = decltype(TC)::value, j0 = decltype(J0C)::value;
             pin(mx[sb]);
             pin(mx2[sb]);
-            if constexpr (decltype(MASKC)::value) {
+            if constexpr (decltype(MASKC)::value && !PW_X_NOMASK) {
                 // key kv0 + c (c = 32t + (j&3) + 8(j>>2) + 4hh) is admissible iff c ∈ [lo, hi]
                 const int lo = (window >= 0 ? qi[sb] - window : -0x40000000) - kv0 - 4 * hh;
                 const int hi = min(window >= 0 ? qi[sb] + window : 0x3fffffff, Sk - 1) - kv0 - 4 * hh;

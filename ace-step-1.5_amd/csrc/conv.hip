@@ -1208,6 +1208,9 @@ __device__ __forceinline__ void ru8_w(const ResUnitArgs &u, uint32_t slot, int k
 #ifndef RU8_X_NOSTORE_S
 #define RU8_X_NOSTORE_S 0
 #endif
+#ifndef RU8_X_NOLOADX
+#define RU8_X_NOLOADX 0    // the residual rows not loaded (zeros): what their re-read from beyond L2 costs
+#endif
 // SIN window helper H (H = 0 / 1: pieces q ≡ H mod 2): global 16-B loads of raw x into registers,
 // Snake (the unit's first, sa_in / sib_in), bf16, LDS — the same image the LDS-DMA would write
 // from x_s.  Plain loads: hipcc counts them and waits for the data of step s only where step
@@ -1448,7 +1451,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             for (int jp = 0; jp < 4; ++jp) {
                 const int r = (int)min((int64_t)(64 * wave + 16 * i + fr), a.M - 1 - mx);
                 const uint32_t off = (uint32_t)(r * 128 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8) * 2;
-                xv[i][jp] = *(const u32x4 *)(xb + off);
+                xv[i][jp] = RU8_X_NOLOADX ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4 *)(xb + off);
             }
         };
         sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
