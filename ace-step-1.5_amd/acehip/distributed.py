@@ -90,7 +90,7 @@ def init(backend: Optional[str] = None, device: Optional[torch.device] = None):
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("ACEHIP_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {}
         if backend == "nccl" and device is not None:
             kw["device_id"] = device
@@ -108,20 +108,35 @@ def broadcast_condition(tensors: Sequence[torch.Tensor], src: int = 0) -> None:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     for t in tensors:
-        dist.broadcast(t, src=src)
+        c = comm_device(t.device)
+        if c is not None and c != t.device:
+            h = t.to(c)
+            dist.broadcast(h, src=src)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src)
+
+
+def comm_device(device: Optional[torch.device]) -> Optional[torch.device]:
+    """Where collective buffers live: the GPU under RCCL, host memory under gloo (which moves
+    CPU tensors only — the ``ACEHIP_DIST_BACKEND=gloo`` rehearsal of the multi-rank path with
+    several ranks on one GPU)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
 
 
 def max_over_ranks(x: float, device: Optional[torch.device] = None) -> float:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=comm_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier(device: Optional[torch.device] = None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
@@ -131,7 +146,7 @@ def gather_floats(vals: Sequence[float], device: Optional[torch.device] = None) 
     """All ranks' values, rank-major (all_gather; the caller's own list at world 1)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return [float(v) for v in vals]
-    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=comm_device(device))
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [float(x) for o in out for x in o.tolist()]
@@ -171,7 +186,7 @@ class SongParallel:
             ts = list(tensors)
             self._B = next(t.shape[0] for t in ts if t is not None)
             return list(range(self._B)), ts, meta
-        dev = self.device
+        dev, cdev = self.device, comm_device(self.device)
         if self.rank == 0:
             ts = list(tensors)
             B = next(t.shape[0] for t in ts if t is not None)
@@ -179,7 +194,7 @@ class SongParallel:
             hdr = [B, [None if t is None else (tuple(t.shape[1:]), t.dtype) for t in ts], meta]
         else:
             hdr = [None, None, None]
-        dist.broadcast_object_list(hdr, src=0, device=dev)
+        dist.broadcast_object_list(hdr, src=0, device=cdev)
         B, specs, meta = hdr
         k = -(-B // self.world)
         mine = song_assignment(B, self.rank, self.world)
@@ -189,19 +204,19 @@ class SongParallel:
                 parts.append(None)
                 continue
             shape, dtype = spec
-            recv = torch.empty(k, *shape, device=dev, dtype=dtype)
+            recv = torch.empty(k, *shape, device=cdev, dtype=dtype)
             send = None
             if self.rank == 0:
-                full = ts[j].to(dev)
+                full = ts[j].to(cdev)
                 send = []
                 for r in range(self.world):
-                    p = torch.zeros(k, *shape, device=dev, dtype=dtype)
+                    p = torch.zeros(k, *shape, device=cdev, dtype=dtype)
                     idx = song_assignment(B, r, self.world)
                     if idx:
                         p[:len(idx)] = full[idx]
                     send.append(p)
             dist.scatter(recv, send, src=0)
-            parts.append(recv[:len(mine)])
+            parts.append(recv[:len(mine)].to(dev) if dev is not None else recv[:len(mine)])
         self._B = B
         return mine, parts, meta
 
@@ -212,18 +227,19 @@ class SongParallel:
             return t
         B = self._B
         k = -(-B // self.world)
-        buf = torch.zeros(k, *t.shape[1:], device=t.device, dtype=t.dtype)
+        cdev = comm_device(t.device)
+        buf = torch.zeros(k, *t.shape[1:], device=cdev, dtype=t.dtype)
         buf[:t.shape[0]] = t
         parts = [torch.empty_like(buf) for _ in range(self.world)] if self.rank == 0 else None
         dist.gather(buf, parts, dst=0)
         if self.rank != 0:
             return None
-        out = torch.empty(B, *t.shape[1:], device=t.device, dtype=t.dtype)
+        out = torch.empty(B, *t.shape[1:], device=cdev, dtype=t.dtype)
         for r in range(self.world):
             idx = song_assignment(B, r, self.world)
             if idx:
                 out[idx] = parts[r][:len(idx)]
-        return out
+        return out.to(t.device)
 
 
 # sampler keyword arguments forwarded to every rank (the rest of the generate_audio contract,
@@ -295,18 +311,18 @@ class SongParallelPipeline:
     def stop(self) -> None:
         """Rank 0: release ranks looping in :meth:`serve`."""
         if self.sp.world > 1:
-            dist.broadcast_object_list(["stop", None, None], src=0, device=self.sp.device)
+            dist.broadcast_object_list(["stop", None, None], src=0, device=comm_device(self.sp.device))
 
     def _run(self, tensors, meta, allow_stop=False):
         sp = self.sp
         if sp.world > 1 and sp.rank != 0:
             hdr = [None, None, None]
-            dist.broadcast_object_list(hdr, src=0, device=sp.device)     # "go" / "stop"
+            dist.broadcast_object_list(hdr, src=0, device=comm_device(sp.device))     # "go" / "stop"
             if hdr[0] == "stop":
                 assert allow_stop
                 return False
         elif sp.world > 1:
-            dist.broadcast_object_list(["go", None, None], src=0, device=sp.device)
+            dist.broadcast_object_list(["go", None, None], src=0, device=comm_device(sp.device))
         songs, parts, meta = sp.scatter(tensors, meta)
         enc, ctx, noise, src, enc_nc, ctx_nc = parts
         kw = dict(meta)

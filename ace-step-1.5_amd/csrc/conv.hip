@@ -1211,6 +1211,42 @@ __device__ __forceinline__ void ru8_w(const ResUnitArgs &u, uint32_t slot, int k
 #ifndef RU8_X_NOLOADX
 #define RU8_X_NOLOADX 0    // the residual rows not loaded (zeros): what their re-read from beyond L2 costs
 #endif
+// RU8_STAMPS (diagnostic builds only, tools/ru8_stamps.py): shader-clock stamps of each block's
+// second tile (steady state).  Role 0, MFMA wave 0: before / after every K-tile barrier (slots
+// 2kt, 2kt+1), after the K loop (32), after epilogue 2 (33), real time at the tile's first
+// barrier and its end (34, 35).  Role 1, the W helper (SIN wave 4, else helper 0): before / after
+// its pre-barrier vmcnt wait (2kt, 2kt+1) — kept in registers and stored after its last wait, so
+// no store of its own sits among the DMAs its counted waits track.  Role 2, window helper 0 (SIN
+// wave 5): before / after its pre-barrier lgkmcnt wait.
+#ifdef RU8_STAMPS
+constexpr int RST_BLK = 1024, RST_SLOTS = 36, RST_LDS = 4 * RST_SLOTS * 8;   // + a dummy role
+__device__ unsigned long long g_ru8_stamps[RST_BLK * 3 * RST_SLOTS];
+// stamps go to LDS past the kernel's own bytes (an LDS write leaves vmcnt alone, so the helpers'
+// counted waits stay exact); each role copies its slots to global memory as it exits
+__device__ __forceinline__ void ru8_stamp(char *lds, int role, int i, unsigned long long v) {
+    if ((threadIdx.x & 63) == 0) ((unsigned long long *)(lds + ru8::LDS))[role * RST_SLOTS + i] = v;
+}
+__device__ __forceinline__ void ru8_stamp_flush(const char *lds, int role) {
+    if (blockIdx.x < RST_BLK && (threadIdx.x & 63) == 0)
+        for (int i = 0; i < RST_SLOTS; ++i)
+            g_ru8_stamps[(blockIdx.x * 3 + role) * RST_SLOTS + i] =
+                ((const unsigned long long *)(lds + ru8::LDS))[role * RST_SLOTS + i];
+}
+#define RU8_STAMP(role, i, v) ru8_stamp(lds, role, i, v)
+#define RU8_STAMP_FLUSH(role) ru8_stamp_flush(lds, role)
+#else
+constexpr int RST_LDS = 0;
+#define RU8_STAMP(role, i, v) do {} while (0)
+#define RU8_STAMP_FLUSH(role) do {} while (0)
+#endif
+__device__ __forceinline__ unsigned long long ru8_now() {
+#ifdef RU8_STAMPS
+    return __builtin_amdgcn_s_memtime();
+#else
+    return 0;
+#endif
+}
+
 // SIN window helper H (H = 0 / 1: pieces q ≡ H mod 2): global 16-B loads of raw x into registers,
 // Snake (the unit's first, sa_in / sib_in), bf16, LDS — the same image the LDS-DMA would write
 // from x_s.  Plain loads: hipcc counts them and waits for the data of step s only where step
@@ -1247,7 +1283,7 @@ __device__ __forceinline__ void sin_write(char *buf, uint32_t loff, int l3, cons
 template <bool RAW, bool SIN = false>
 __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
     constexpr int RBM = ru8::BM, WINB = ru8::WINB, WT = ru8::WT;
-    __shared__ __attribute__((aligned(16))) char lds[ru8::LDS];
+    __shared__ __attribute__((aligned(16))) char lds[ru8::LDS + RST_LDS];
     const ConvArgs &a = u.c1;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1273,8 +1309,10 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             const bool more = t + 1 < t1;
             sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
                 constexpr int kt = decltype(KT)::value;
+                if (t == t0 + 1) RU8_STAMP(1, 2 * kt, ru8_now());
                 if (more) vm_wait<ru8::w_newer(kt, true)>();
                 else vm_wait<ru8::w_newer(kt, false)>();
+                if (t == t0 + 1) RU8_STAMP(1, 2 * kt + 1, ru8_now());
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 const int sp = slot == 0 ? ru8::NSLOT - 1 : slot - 1;
@@ -1289,6 +1327,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             });
         }
         vm_wait<0>();
+        RU8_STAMP_FLUSH(1);
         return;
     }
     if (SIN && wave >= 5) {
@@ -1328,7 +1367,9 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 const bool first = t == t0, more = t + 1 < t1;
                 sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
                     constexpr int kt = decltype(KT)::value, PB = kt & 1, PP = PB ^ 1;
+                    if (H == 0 && t == t0 + 1) RU8_STAMP(2, 2 * kt, ru8_now());
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's LDS writes landed
+                    if (H == 0 && t == t0 + 1) RU8_STAMP(2, 2 * kt + 1, ru8_now());
                     __builtin_amdgcn_s_barrier();
                     asm volatile("" ::: "memory");
                     // issue step kt's loads into ld[PB] (the ranges of the DMA schedule)
@@ -1356,6 +1397,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 });
             }
             vm_wait<0>();
+            if (H == 0) RU8_STAMP_FLUSH(2);
         };
         if (wave == 5) run(IC7<0>{});
         else run(IC7<1>{});
@@ -1379,6 +1421,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             const bool first = t == t0, more = t + 1 < t1;
             sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
                 constexpr int kt = decltype(KT)::value;
+                if (h == 0 && t == t0 + 1) RU8_STAMP(1, 2 * kt, ru8_now());
                 // pre-barrier kt: W(kt) and everything issued before it landed
                 if (h == 0) {
                     if (first) {
@@ -1397,6 +1440,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                         else vm_wait<ru8::allowed(kt, 1, false, false)>();
                     }
                 }
+                if (h == 0 && t == t0 + 1) RU8_STAMP(1, 2 * kt + 1, ru8_now());
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 // step kt: window pieces, then W
@@ -1416,6 +1460,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             });
         }
         vm_wait<0>();
+        if (h == 0) RU8_STAMP_FLUSH(1);
         return;
     }
 
@@ -1454,10 +1499,22 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 xv[i][jp] = RU8_X_NOLOADX ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4 *)(xb + off);
             }
         };
+#ifdef RU8_STAMPS
+        // MFMA-wave stamps without a branch (a branch per K-tile broke the unrolled schedule and
+        // spilled): every lane of every MFMA wave writes; only wave 0's steady tile to role 0
+        unsigned long long *sb = (unsigned long long *)(lds + ru8::LDS) + (wave == 0 && t == t0 + 1 ? 0 : 3 * RST_SLOTS);
+#endif
         sfor<0, 16>([&](auto KT) __attribute__((always_inline)) {
             constexpr int kt = decltype(KT)::value;
+#ifdef RU8_STAMPS
+            sb[2 * kt] = ru8_now();
+#endif
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+#ifdef RU8_STAMPS
+            sb[2 * kt + 1] = ru8_now();
+            if constexpr (kt == 0) sb[34] = __builtin_amdgcn_s_memrealtime();
+#endif
             // (slot opaque: with 16 % NSLOT == 0 hipcc folds every K-tile's slot to a constant and
             // hoists the 16 fragment bases out of the tile loop, where they spill)
             asm volatile("" : "+s"(slot));
@@ -1539,6 +1596,9 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 }
             }
         });
+#ifdef RU8_STAMPS
+        sb[32] = ru8_now();
+#endif
         // epilogue 2: x' = x + bf16(acc + b2) (raw, optional) and snake_next(x') → out_s
         int64_t me = m0;
         asm volatile("" : "+s"(me));
@@ -1580,7 +1640,12 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 }
             }
         }
+#ifdef RU8_STAMPS
+        sb[33] = ru8_now();
+        sb[35] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
+    if (wave == 0) RU8_STAMP_FLUSH(0);
 }
 
 __global__ void permute_k1_kernel(const bf16_t *w, bf16_t *wp, int n_rows) {
@@ -1974,3 +2039,16 @@ int cast_bf16_f32(const bf16_t *src, float *dst, int64_t n, hipStream_t s) {
 }
 
 }  // namespace acehip
+
+#ifdef RU8_STAMPS
+extern "C" int acehip_diag_ru8_stamps(void *host) {
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(acehip::g_ru8_stamps), sizeof(acehip::g_ru8_stamps)));
+    return 0;
+}
+extern "C" int acehip_diag_ru8_stamps_clear(void) {
+    void *p = nullptr;
+    HIP_TRY(hipGetSymbolAddress(&p, HIP_SYMBOL(acehip::g_ru8_stamps)));
+    HIP_TRY(hipMemset(p, 0, sizeof(acehip::g_ru8_stamps)));
+    return 0;
+}
+#endif

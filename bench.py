@@ -232,8 +232,12 @@ def main():
     from acehip.flops import dit_flops_executed_cfg_song_step, dit_flops_per_row, vae_decoder_flops
     from acehip.provenance import product_hash
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gi = local
+    if os.environ.get("ACEHIP_DIST_BACKEND") == "gloo":
+        # rehearsal of the multi-rank path on fewer GPUs than ranks (gloo, host-staged collectives)
+        gi = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gi)
+    dev = torch.device("cuda", gi)
     D.init(device=dev)
 
     T = int(round(args.seconds * 25))
@@ -248,13 +252,13 @@ def main():
     # random-init weights of the real architecture, identical on every rank
     W = synth_dit_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch")
     null = synth_null_condition(cfg, seed=0, device=dev, dtype=torch.bfloat16, backend="torch")
-    rt = DiTRuntime(cfg, local, max_S=S, max_Bc=Bc, max_Lenc=args.lenc)
+    rt = DiTRuntime(cfg, gi, max_S=S, max_Bc=Bc, max_Lenc=args.lenc)
     rt.load(W)
     rt.use_graph(args.graph)
     prep = None
     if not args.no_condition:
         # lyric + timbre + text encoders on the HIP path; Lenc = lyric + 1 timbre + text
-        ce = ConditionEncoder(cfg, local, max_batch=world, max_lyric=args.lyric_len, max_refs=world,
+        ce = ConditionEncoder(cfg, gi, max_batch=world, max_lyric=args.lyric_len, max_refs=world,
                               max_ref_frames=750)
         ce.load(synth_condenc_weights(cfg, seed=0, mode="bench", device=dev, dtype=torch.bfloat16, backend="torch"))
         prep = HipPrepareCondition(ce)
@@ -262,7 +266,7 @@ def main():
         # the Qwen3-Embedding-0.6B text encoder (infer_text_embeddings / infer_lyric_embeddings,
         # conditioning_embed.py:71-79): 28 causal layers for the text tokens, the table for lyrics
         te_cfg = DiTConfig(**TextEncoder.QWEN3_06B)
-        te = TextEncoder(te_cfg, local, max_batch=world, max_tokens=max(args.text_len, 64),
+        te = TextEncoder(te_cfg, gi, max_batch=world, max_tokens=max(args.text_len, 64),
                          overlap=not args.no_overlap)
         te.load(synth_text_encoder_weights(te_cfg, QWEN3_VOCAB, seed=0, mode="bench", device=dev,
                                            dtype=torch.bfloat16, backend="torch"))
@@ -271,7 +275,7 @@ def main():
     if not args.no_vae:
         vae_w = synth_vae_weights(vcfg, seed=0, mode="bench", with_encoder=args.repaint, device=dev,
                                   dtype=torch.bfloat16, backend="torch")
-        vae = OobleckBackend(vcfg, local, max_T=T, with_encoder=args.repaint)
+        vae = OobleckBackend(vcfg, gi, max_T=T, with_encoder=args.repaint)
         vae.load(vae_w)
 
     # synthetic conditioning on rank 0, broadcast over RCCL; the
