@@ -41,12 +41,39 @@ __device__ __forceinline__ const bf16_t *a_src(const ConvArgs &a, int64_t m, int
     return a.in + pos * a.Cin + ci0 + c * 8;
 }
 
-// Snake of a value already rounded to bf16: x + 1/(e^β+1e-9)·sin(e^α x)²
-// (v_sin_f32 via __sinf: |α·x| stays small for Oobleck activations, and the
+// Snake of a value already rounded to bf16: x + 1/(e^β+1e-9)·sin(e^α x)².  `a` is e^α/(2π)
+// (snake_params_kernel folds the 1/(2π) in): v_sin_f32 takes its argument in revolutions, so
+// the sine is one multiply and one v_sin (|α·x| stays small for Oobleck activations, and the
 // result is rounded to bf16 anyway)
 __device__ __forceinline__ float snake1(float x, float a, float ib) {
-    const float s = __sinf(a * x);
-    return x + ib * s * s;
+    const float s = __builtin_amdgcn_sinf(a * x);
+    return __builtin_fmaf(ib * s, s, x);
+}
+// the same on a pair (v_pk_mul_f32 / v_pk_fma_f32: two values per VALU slot; IEEE-identical
+// to two snake1 calls)
+__device__ __forceinline__ f32x2 snake2(f32x2 x, f32x2 a, f32x2 ib) {
+    const f32x2 t = a * x;
+    const f32x2 s = {__builtin_amdgcn_sinf(t.x), __builtin_amdgcn_sinf(t.y)};
+    return __builtin_elementwise_fma(ib * s, s, x);
+}
+// array forms over pairs (N even): y = snake(x), o += v
+template <int N>
+__device__ __forceinline__ void snake_n(const float *x, const float *a, const float *ib, float *y) {
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = snake2(f32x2{x[i], x[i + 1]}, f32x2{a[i], a[i + 1]}, f32x2{ib[i], ib[i + 1]});
+        y[i] = r.x;
+        y[i + 1] = r.y;
+    }
+}
+template <int N>
+__device__ __forceinline__ void add_n(float *o, const float *v) {
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = f32x2{o[i], o[i + 1]} + f32x2{v[i], v[i + 1]};
+        o[i] = r.x;
+        o[i + 1] = r.y;
+    }
 }
 
 // snake1 over 8 channels with 16-B parameter loads (sa / sib fp32 per channel)
@@ -55,8 +82,7 @@ __device__ __forceinline__ void snake8(const float (&x)[8], const float *sa, con
     const float4 b0 = *(const float4 *)sib, b1 = *(const float4 *)(sib + 4);
     const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-    for (int r = 0; r < 8; ++r) y[r] = snake1(x[r], av[r], bv[r]);
+    snake_n<8>(x, av, bv, y);
 }
 
 // Both operands by global_load_lds into a 2-stage ring: [A im2col rows | W rows],
@@ -146,16 +172,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
             if (a.bias) {
                 float bb[8];
                 unpack8(*(const uint4 *)(a.bias + n), bb);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                add_n<8>(o, bb);
             }
-#pragma unroll
-            for (int r = 0; r < 8; ++r) o[r] = rbf(o[r]);                    // conv output (bf16)
+            rbf_n<8>(o);                                                     // conv output (bf16)
             if constexpr (RES) {
                 float rr[8];
                 unpack8(*(const uint4 *)(a.res + row * a.N + n), rr);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + o[r]);
+                add_n<8>(o, rr);
+                rbf_n<8>(o);
             }
             if constexpr (RAW) *(uint4 *)(a.out + row * a.N + n) = pack8(o);
             if constexpr (SN) {
@@ -374,19 +398,18 @@ __global__ __launch_bounds__(512, 1) void convp_kernel(ConvArgs a, int64_t nitem
             const int rl = wm * TM + i * 16 + fr;
             const int64_t m = m0 + rl;
             const int64_t row = m * a.c_stride + a.c_off + phase;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) o[r] = rbf(o[r] + bb[r]);
+            add_n<8>(o, bb);
+            rbf_n<8>(o);
             if constexpr (RES) {
                 float rr[8];
                 const int cl = (n - n0) >> 3;           // 16-B chunk of the item's 128 columns
                 unpack8(*(const uint4 *)(resb + rl * 256 + ((cl ^ (rl & 15)) << 4)), rr);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + o[r]);
+                add_n<8>(o, rr);
+                rbf_n<8>(o);
             }
             float sn[8];
             if constexpr (SN) {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) sn[r] = snake1(o[r], psa[n + r], psib[n + r]);
+                snake_n<8>(o, psa + n, psib + n, sn);
             }
             if (m < a.M && row >= 0 && row < a.L_out) {
                 if constexpr (RAW) *(uint4 *)(a.out + row * a.N + n) = pack8(o);
@@ -491,8 +514,10 @@ __global__ __launch_bounds__(256, 2) void resunit128_kernel(ResUnitArgs u) {
             const float4 sb = *(const float4 *)(a.sib + n);
             const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
             float o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + bb[r]), sav[r], sbv[r]);
+            float t[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            add_n<4>(t, bb);
+            rbf_n<4>(t);
+            snake_n<4>(t, sav, sbv, o);
             const int h = n >> 6, cc = (n & 63) >> 3;
             *(uint2 *)(ys + h * 16384 + swz(row, cc) + (n & 7) * 2) = pack4(o);
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -531,8 +556,10 @@ __global__ __launch_bounds__(256, 2) void resunit128_kernel(ResUnitArgs u) {
             const int n = wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
             unpack8(*(const uint4 *)(u.b2 + n), bb);
             unpack8(*(const uint4 *)(u.x + m * 128 + n), rr);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+            add_n<8>(o, bb);
+            rbf_n<8>(o);
+            add_n<8>(o, rr);
+            rbf_n<8>(o);
             if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
             float sn[8];
             snake8(o, u.sa_next + n, u.sib_next + n, sn);
@@ -692,11 +719,9 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(Conv
                 if (a.bias) {
                     float bb[8];
                     unpack8(*(const uint4 *)(a.bias + n), bb);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                    add_n<8>(o, bb);
                 }
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] = rbf(o[r]);
+                rbf_n<8>(o);
                 float sn[8];
                 snake8(o, a.sa + n, a.sib + n, sn);
                 *(uint4 *)(a.out_s + m * a.N + n) = pack8(sn);
@@ -732,8 +757,10 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(Conv
                 const float4 sb = *(const float4 *)(a.sib + n);
                 const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
                 float o[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + bb[r]), sav[r], sbv[r]);
+                float t[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                add_n<4>(t, bb);
+                rbf_n<4>(t);
+                snake_n<4>(t, sav, sbv, o);
                 const int h = n >> 6, cc = (n & 63) >> 3;
                 *(uint2 *)(ys + h * YH + sw7(row, cc) + (n & 7) * 2) = pack4(o);
                 acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -771,8 +798,10 @@ __global__ __launch_bounds__(BM_ * 2, BM_ == 256 ? 1 : 2) void conv7_kernel(Conv
                 const int n = wn * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + (fc >> 1) * 8;
                 unpack8(b2v[jp], bb);
                 unpack8(xv[i][jp], rr);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
+                add_n<8>(o, bb);
+                rbf_n<8>(o);
+                add_n<8>(o, rr);
+                rbf_n<8>(o);
                 if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
                 float sn[8];
                 snake8(o, u.sa_next + n, u.sib_next + n, sn);
@@ -1003,8 +1032,10 @@ __global__ __launch_bounds__(256, 2) void ru7_kernel(ResUnitArgs u, int64_t ntil
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
                         float o[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + b[r]), sav[r], sbv[r]);
+                        float t[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                        add_n<4>(t, b);
+                        rbf_n<4>(t);
+                        snake_n<4>(t, sav, sbv, o);
                         yv[i][j] = pack4(o);
                         acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                     }
@@ -1052,11 +1083,11 @@ __global__ __launch_bounds__(256, 2) void ru7_kernel(ResUnitArgs u, int64_t ntil
                 acc[i][2 * jp] = f32x4{0.f, 0.f, 0.f, 0.f};
                 acc[i][2 * jp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 unpack8(make_uint4(xv[i][jp].x, xv[i][jp].y, xv[i][jp].z, xv[i][jp].w), rr);
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
-                    sn[r] = snake1(o[r], av[r], sv[r]);
-                }
+                add_n<8>(o, bb);
+                rbf_n<8>(o);
+                add_n<8>(o, rr);
+                rbf_n<8>(o);
+                snake_n<8>(o, av, sv, sn);
                 const int64_t m = me + 32 * wave + 16 * i + fr;
                 if (m < a.M) {
                     if constexpr (RAW) *(uint4 *)(u.x + m * 128 + n) = pack8(o);
@@ -1211,6 +1242,24 @@ __device__ __forceinline__ void ru8_w(const ResUnitArgs &u, uint32_t slot, int k
 #ifndef RU8_X_NOLOADX
 #define RU8_X_NOLOADX 0    // the residual rows not loaded (zeros): what their re-read from beyond L2 costs
 #endif
+// SIN window rows: loaded RU8_WLEAD helper steps before their Snake + LDS write (2: the rows come
+// from HBM — the previous unit's output — and one step, ≈ 0.6 µs, left the helpers waiting on
+// them at most barriers; 1: the previous schedule, A/B).  Deadlines with lead 2: chunk 1 of a tile
+// written by step 5 (read from K-tile 7), chunk 0 of the next by step 14 (read from K-tile 0'),
+// the first part of its chunk 1 at steps 0' / 1' (buffer 1 free since K-tile 13)
+#ifndef RU8_WLEAD
+#define RU8_WLEAD 2
+#endif
+// window helpers' Snake in packed f32 (v_pk_mul / v_pk_fma) or scalar: the helpers issue beside
+// an MFMA wave on their SIMD, where the guide prices packed f32 VALU as an anti-lever
+#ifndef RU8_WPACKED
+#define RU8_WPACKED 0
+#endif
+// residual prefetch distance in row fragments: fragment i's x rows are loaded while fragment
+// i − RU8_XDIST is in epilogue 2 (the first RU8_XDIST during K-tile 15)
+#ifndef RU8_XDIST
+#define RU8_XDIST 2
+#endif
 // RU8_STAMPS (diagnostic builds only, tools/ru8_stamps.py): shader-clock stamps of each block's
 // second tile (steady state).  Role 0, MFMA wave 0: before / after every K-tile barrier (slots
 // 2kt, 2kt+1), after the K loop (32), after epilogue 2 (33), real time at the tile's first
@@ -1247,17 +1296,33 @@ __device__ __forceinline__ unsigned long long ru8_now() {
 #endif
 }
 
-// SIN window helper H (H = 0 / 1: pieces q ≡ H mod 2): global 16-B loads of raw x into registers,
+// SIN window helpers: RU8_NWH waves (one per SIMD beside its MFMA wave with the W helper on the
+// fourth; the stamps showed two helpers' Snake VALU arriving 700-1450 cycles after the MFMA waves
+// at most K-tile barriers).  RU8_NWH=2 (A/B): the previous two.
+#ifndef RU8_NWH
+#define RU8_NWH 3
+#endif
+namespace ru8 {
+constexpr int NWH = RU8_NWH;
+static_assert(NWH == 2 || NWH == 3, "window helpers");
+}  // namespace ru8
+// SIN window helper H (pieces q ≡ H mod NWH): global 16-B loads of raw x into registers,
 // Snake (the unit's first, sa_in / sib_in), bf16, LDS — the same image the LDS-DMA would write
 // from x_s.  Plain loads: hipcc counts them and waits for the data of step s only where step
 // s + 1 writes it out (inline-asm loads would leave a register copy of an unlanded destination
 // possible between the load and its wait).
+__host__ __device__ constexpr int win_share(int p0, int p1, int h) {
+    int n = 0;
+    for (int q = p0; q < p1; ++q) n += q % ru8::NWH == h;
+    return n;
+}
 template <int H, int P0, int P1>
 __device__ __forceinline__ void sin_issue(const char *src, uint32_t goff, int l3, uint4 (&ld)[4]) {
+    static_assert(win_share(P0, P1, H) <= 4, "a helper's pieces per step fit its load registers");
     int k = 0;
 #pragma unroll
     for (int q = P0; q < P1; ++q) {
-        if ((q & 1) != H) continue;
+        if (q % ru8::NWH != H) continue;
         if (q * 8 + 8 <= ru8::WROWS || l3 < ru8::WROWS - q * 8) ld[k] = *(const uint4 *)(src + (int64_t)q * 8 * 256 + goff);
         ++k;
     }
@@ -1268,12 +1333,16 @@ __device__ __forceinline__ void sin_write(char *buf, uint32_t loff, int l3, cons
     int k = 0;
 #pragma unroll
     for (int q = P0; q < P1; ++q) {
-        if ((q & 1) != H) continue;
+        if (q % ru8::NWH != H) continue;
         if (q * 8 + 8 <= ru8::WROWS || l3 < ru8::WROWS - q * 8) {
             float x[8], y[8];
             unpack8(ld[k], x);
+            if (RU8_WPACKED) {
+                snake_n<8>(x, sa, sb, y);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) y[e] = snake1(x[e], sa[e], sb[e]);
+                for (int e = 0; e < 8; ++e) y[e] = snake1(x[e], sa[e], sb[e]);
+            }
             *(uint4 *)(buf + q * 1024 + loff) = pack8(y);
         }
         ++k;
@@ -1281,7 +1350,7 @@ __device__ __forceinline__ void sin_write(char *buf, uint32_t loff, int l3, cons
 }
 
 template <bool RAW, bool SIN = false>
-__global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
+__global__ __launch_bounds__(SIN ? 320 + 64 * ru8::NWH : 384, 1) void ru8_kernel(ResUnitArgs u, int64_t ntiles) {
     constexpr int RBM = ru8::BM, WINB = ru8::WINB, WT = ru8::WT;
     __shared__ __attribute__((aligned(16))) char lds[ru8::LDS + RST_LDS];
     const ConvArgs &a = u.c1;
@@ -1372,6 +1441,21 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                     if (H == 0 && t == t0 + 1) RU8_STAMP(2, 2 * kt + 1, ru8_now());
                     __builtin_amdgcn_s_barrier();
                     asm volatile("" ::: "memory");
+                    auto fin = [&](auto P0C, auto P1C, auto CCC, auto BC) __attribute__((always_inline)) {
+                        constexpr int p0 = decltype(P0C)::value, p1 = decltype(P1C)::value, cc = decltype(CCC)::value;
+                        sin_write<H, p0, p1>(win + cc * WINB, loff, l3, ld[decltype(BC)::value], sa[cc], sb[cc]);
+                    };
+                    if constexpr (RU8_WLEAD == 2) {
+                        // finish step kt − 2's pieces (Snake, LDS) first: they sit in ld[PB], the
+                        // registers step kt issues into next — two steps for their rows to arrive
+                        if constexpr (kt >= 2 && kt <= 5) {          // chunk 1 of this tile
+                            if (!first) fin(IC7<ru8::c1b_lo(kt - 2)>{}, IC7<ru8::c1b_hi(kt - 2)>{}, IC7<1>{}, IC7<PB>{});
+                        } else if constexpr (kt >= 9 && kt <= 14) {  // chunk 0 of the next tile
+                            if (more) fin(IC7<ru8::c0_lo(kt - 9)>{}, IC7<ru8::c0_hi(kt - 9)>{}, IC7<0>{}, IC7<PB>{});
+                        } else if constexpr (kt <= 1) {              // issued at steps 14 / 15 of the previous tile
+                            if (!first) fin(IC7<ru8::c1a_lo(kt)>{}, IC7<ru8::c1a_hi(kt)>{}, IC7<1>{}, IC7<PB>{});
+                        }
+                    }
                     // issue step kt's loads into ld[PB] (the ranges of the DMA schedule)
                     if constexpr (kt <= 3) {
                         if (!first) sin_issue<H, ru8::c1b_lo(kt), ru8::c1b_hi(kt)>(src_of(m0, 1), goff, l3, ld[PB]);
@@ -1380,19 +1464,17 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                     } else if constexpr (kt >= 14) {
                         if (more) sin_issue<H, ru8::c1a_lo(kt - 14), ru8::c1a_hi(kt - 14)>(src_of(m0 + RBM, 1), goff, l3, ld[PB]);
                     }
-                    // finish step kt − 1's pieces (loaded into ld[PP]): Snake, LDS
-                    auto fin = [&](auto P0C, auto P1C, auto CCC) __attribute__((always_inline)) {
-                        constexpr int p0 = decltype(P0C)::value, p1 = decltype(P1C)::value, cc = decltype(CCC)::value;
-                        sin_write<H, p0, p1>(win + cc * WINB, loff, l3, ld[PP], sa[cc], sb[cc]);
-                    };
-                    if constexpr (kt >= 1 && kt <= 4) {          // chunk 1 of this tile, issued at kt − 1
-                        if (!first) fin(IC7<ru8::c1b_lo(kt - 1)>{}, IC7<ru8::c1b_hi(kt - 1)>{}, IC7<1>{});
-                    } else if constexpr (kt >= 8 && kt <= 13) {  // chunk 0 of the next tile
-                        if (more) fin(IC7<ru8::c0_lo(kt - 8)>{}, IC7<ru8::c0_hi(kt - 8)>{}, IC7<0>{});
-                    } else if constexpr (kt == 15) {             // chunk 1 (first part) of the next tile
-                        if (more) fin(IC7<ru8::c1a_lo(0)>{}, IC7<ru8::c1a_hi(0)>{}, IC7<1>{});
-                    } else if constexpr (kt == 0) {              // issued at step 15 of the previous tile
-                        if (!first) fin(IC7<ru8::c1a_lo(1)>{}, IC7<ru8::c1a_hi(1)>{}, IC7<1>{});
+                    if constexpr (RU8_WLEAD == 1) {
+                        // finish step kt − 1's pieces (loaded into ld[PP]): Snake, LDS
+                        if constexpr (kt >= 1 && kt <= 4) {          // chunk 1 of this tile, issued at kt − 1
+                            if (!first) fin(IC7<ru8::c1b_lo(kt - 1)>{}, IC7<ru8::c1b_hi(kt - 1)>{}, IC7<1>{}, IC7<PP>{});
+                        } else if constexpr (kt >= 8 && kt <= 13) {  // chunk 0 of the next tile
+                            if (more) fin(IC7<ru8::c0_lo(kt - 8)>{}, IC7<ru8::c0_hi(kt - 8)>{}, IC7<0>{}, IC7<PP>{});
+                        } else if constexpr (kt == 15) {             // chunk 1 (first part) of the next tile
+                            if (more) fin(IC7<ru8::c1a_lo(0)>{}, IC7<ru8::c1a_hi(0)>{}, IC7<1>{}, IC7<PP>{});
+                        } else if constexpr (kt == 0) {              // issued at step 15 of the previous tile
+                            if (!first) fin(IC7<ru8::c1a_lo(1)>{}, IC7<ru8::c1a_hi(1)>{}, IC7<1>{}, IC7<PP>{});
+                        }
                     }
                 });
             }
@@ -1400,7 +1482,8 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
             if (H == 0) RU8_STAMP_FLUSH(2);
         };
         if (wave == 5) run(IC7<0>{});
-        else run(IC7<1>{});
+        else if (ru8::NWH == 2 || wave == 6) run(IC7<1>{});
+        else run(IC7<2>{});
         return;
     }
     if (!SIN && wave >= 4) {
@@ -1559,8 +1642,10 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                         const float4 sa = *(const float4 *)(psa2 + n), sb = *(const float4 *)(psib2 + n);
                         const float sav[4] = {sa.x, sa.y, sa.z, sa.w}, sbv[4] = {sb.x, sb.y, sb.z, sb.w};
                         float o[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = snake1(rbf(acc[i][j][r] + b[r]), sav[r], sbv[r]);
+                        float t[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                        add_n<4>(t, b);
+                        rbf_n<4>(t);
+                        snake_n<4>(t, sav, sbv, o);
                         yv[j] = pack4(o);
                         acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                     }
@@ -1594,6 +1679,8 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                         for (int i = 0; i < 4; ++i)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], yk[i][ks], acc[i][j], 0, 0, 0);
                 }
+#pragma unroll
+                for (int i = 1; i < RU8_XDIST; ++i) load_x(i);
             }
         });
 #ifdef RU8_STAMPS
@@ -1604,7 +1691,7 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
         asm volatile("" : "+s"(me));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            if (i < 3) load_x(i + 1);     // lands during fragment i's epilogue
+            if (i + RU8_XDIST < 4) load_x(i + RU8_XDIST);     // lands during the epilogues before its own
             int pl2 = (odd ? 16 : 0) + (fc >> 1) * 8;
             asm volatile("" : "+v"(pl2));
 #pragma unroll
@@ -1621,10 +1708,17 @@ __global__ __launch_bounds__(SIN ? 448 : 384, 1) void ru8_kernel(ResUnitArgs u, 
                 acc[i][2 * jp] = f32x4{0.f, 0.f, 0.f, 0.f};
                 acc[i][2 * jp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 unpack8(make_uint4(xv[i][jp].x, xv[i][jp].y, xv[i][jp].z, xv[i][jp].w), rr);
+                add_n<8>(o, bb);
+                rbf_n<8>(o);
+                add_n<8>(o, rr);
+                rbf_n<8>(o);
+                if constexpr (!(SIN && RAW)) {
+                    if (RU8_X_NOSNAKE2) {
 #pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    o[r] = rbf(rr[r] + rbf(o[r] + bb[r]));
-                    if constexpr (!(SIN && RAW)) sn[r] = RU8_X_NOSNAKE2 ? o[r] : snake1(o[r], av[r], sv[r]);
+                        for (int r = 0; r < 8; ++r) sn[r] = o[r];
+                    } else {
+                        snake_n<8>(o, av, sv, sn);
+                    }
                 }
                 const int64_t m = me + 64 * wave + 16 * i + fr;
                 if (m < a.M) {
@@ -1841,7 +1935,7 @@ __global__ void fuse_conv_f32_kernel(const bf16_t *v, const bf16_t *g, int d0, i
 __global__ void snake_params_kernel(const bf16_t *alpha, const bf16_t *beta, int C, float *sa, float *sib) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    sa[c] = expf(bf2f(alpha[c]));
+    sa[c] = expf(bf2f(alpha[c])) * 0.15915494309189535f;   // e^α / (2π): snake1's sine in revolutions
     sib[c] = 1.0f / (expf(bf2f(beta[c])) + 1e-9f);
 }
 
@@ -1946,8 +2040,8 @@ int resunit128(const ResUnitArgs &u, hipStream_t s) {
         if (u.snake_in) {
             if (!u.sa_in || !u.sib_in || (u.keep_raw && (!u.x_out || u.x_out == u.x)) || a.in != u.x)
                 return fail(-1, "resunit128: snake_in needs sa_in / sib_in, in == x and a separate x_out");
-            if (u.keep_raw) ru8_kernel<true, true><<<nb, 448, 0, s>>>(u, nt);
-            else ru8_kernel<false, true><<<nb, 448, 0, s>>>(u, nt);
+            if (u.keep_raw) ru8_kernel<true, true><<<nb, 320 + 64 * ru8::NWH, 0, s>>>(u, nt);
+            else ru8_kernel<false, true><<<nb, 320 + 64 * ru8::NWH, 0, s>>>(u, nt);
         } else if (u.keep_raw) {
             ru8_kernel<true><<<nb, 384, 0, s>>>(u, nt);
         } else {
