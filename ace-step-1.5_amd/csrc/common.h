@@ -60,6 +60,41 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 // VALU-bound and the result is rounded to bf16 right after
 __device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// Snake of a value already rounded to bf16: x + 1/(e^β+1e-9)·sin(e^α x)².  `a` is e^α/(2π)
+// (snake_params_kernel folds the 1/(2π) in): v_sin_f32 takes its argument in revolutions, so
+// the sine is one multiply and one v_sin (|α·x| stays small for Oobleck activations, and the
+// result is rounded to bf16 anyway)
+__device__ __forceinline__ float snake1(float x, float a, float ib) {
+    const float s = __builtin_amdgcn_sinf(a * x);
+    return __builtin_fmaf(ib * s, s, x);
+}
+// the same on a pair (v_pk_mul_f32 / v_pk_fma_f32: two values per VALU slot; IEEE-identical
+// to two snake1 calls)
+__device__ __forceinline__ f32x2 snake2(f32x2 x, f32x2 a, f32x2 ib) {
+    const f32x2 t = a * x;
+    const f32x2 s = {__builtin_amdgcn_sinf(t.x), __builtin_amdgcn_sinf(t.y)};
+    return __builtin_elementwise_fma(ib * s, s, x);
+}
+// array forms over pairs (N even): y = snake(x), o += v
+template <int N>
+__device__ __forceinline__ void snake_n(const float *x, const float *a, const float *ib, float *y) {
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = snake2(f32x2{x[i], x[i + 1]}, f32x2{a[i], a[i + 1]}, f32x2{ib[i], ib[i + 1]});
+        y[i] = r.x;
+        y[i + 1] = r.y;
+    }
+}
+template <int N>
+__device__ __forceinline__ void add_n(float *o, const float *v) {
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = f32x2{o[i], o[i + 1]} + f32x2{v[i], v[i + 1]};
+        o[i] = r.x;
+        o[i + 1] = r.y;
+    }
+}
+
 // pack/unpack 8 bf16 in a uint4
 __device__ __forceinline__ void unpack8(const uint4 &u, float *f) {
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};

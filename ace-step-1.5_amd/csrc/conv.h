@@ -5,7 +5,7 @@
 namespace acehip {
 
 // out[m·c_stride + c_off + phase][n] = Σ_{tap,ci} in[m·a_stride + tap·dil + a_off][ci] · W_phase[n][tap·Cin + ci] (+bias[n]) (+res)
-// epilogue writes the raw value to `out` and/or Snake(raw) (params sa = e^α,
+// epilogue writes the raw value to `out` and/or Snake(raw) (params sa = e^α/(2π),
 // sib = 1/(e^β+1e-9)) to `out_s` — the activation the NEXT convolution consumes.
 struct ConvArgs {
     const bf16_t *in; int64_t L_in; int Cin;     // NLC input [L_in][Cin]
@@ -18,6 +18,10 @@ struct ConvArgs {
     int64_t M;                                   // GEMM rows per phase
     int taps, dil, a_stride, a_off, c_stride, c_off;
     const bf16_t *zero;                          // ≥ 128 B of zeros (im2col padding source)
+    // in is a VAE activation buffer: ≥ kActPadRows zero rows before row 0 and addressable rows
+    // after L_in (the k = 7 conv may then run as an implicit GEMM on the ping-pong tile, which
+    // reads its halo rows from there; ACEHIP_CONV7=2)
+    int in_halo = 0;
 };
 // fused residual unit at C = 128: c1 = the k=7 conv (in = x_s, sa/sib = snake2,
 // bias = b1); then x' = x + (W2·y_s + b2), written raw into x (keep_raw) and

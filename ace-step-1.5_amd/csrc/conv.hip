@@ -41,41 +41,6 @@ __device__ __forceinline__ const bf16_t *a_src(const ConvArgs &a, int64_t m, int
     return a.in + pos * a.Cin + ci0 + c * 8;
 }
 
-// Snake of a value already rounded to bf16: x + 1/(e^β+1e-9)·sin(e^α x)².  `a` is e^α/(2π)
-// (snake_params_kernel folds the 1/(2π) in): v_sin_f32 takes its argument in revolutions, so
-// the sine is one multiply and one v_sin (|α·x| stays small for Oobleck activations, and the
-// result is rounded to bf16 anyway)
-__device__ __forceinline__ float snake1(float x, float a, float ib) {
-    const float s = __builtin_amdgcn_sinf(a * x);
-    return __builtin_fmaf(ib * s, s, x);
-}
-// the same on a pair (v_pk_mul_f32 / v_pk_fma_f32: two values per VALU slot; IEEE-identical
-// to two snake1 calls)
-__device__ __forceinline__ f32x2 snake2(f32x2 x, f32x2 a, f32x2 ib) {
-    const f32x2 t = a * x;
-    const f32x2 s = {__builtin_amdgcn_sinf(t.x), __builtin_amdgcn_sinf(t.y)};
-    return __builtin_elementwise_fma(ib * s, s, x);
-}
-// array forms over pairs (N even): y = snake(x), o += v
-template <int N>
-__device__ __forceinline__ void snake_n(const float *x, const float *a, const float *ib, float *y) {
-#pragma unroll
-    for (int i = 0; i < N; i += 2) {
-        const f32x2 r = snake2(f32x2{x[i], x[i + 1]}, f32x2{a[i], a[i + 1]}, f32x2{ib[i], ib[i + 1]});
-        y[i] = r.x;
-        y[i + 1] = r.y;
-    }
-}
-template <int N>
-__device__ __forceinline__ void add_n(float *o, const float *v) {
-#pragma unroll
-    for (int i = 0; i < N; i += 2) {
-        const f32x2 r = f32x2{o[i], o[i + 1]} + f32x2{v[i], v[i + 1]};
-        o[i] = r.x;
-        o[i + 1] = r.y;
-    }
-}
-
 // snake1 over 8 channels with 16-B parameter loads (sa / sib fp32 per channel)
 __device__ __forceinline__ void snake8(const float (&x)[8], const float *sa, const float *sib, float (&y)[8]) {
     const float4 a0 = *(const float4 *)sa, a1 = *(const float4 *)(sa + 4);
@@ -1987,8 +1952,23 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
     if (!a.out && !a.out_s) return fail(-1, "conv_gemm: no output");
     if (!a.zero) return fail(-1, "conv_gemm: zero page");
     if (a.out_s && (!a.sa || !a.sib)) return fail(-1, "conv_gemm: snake params");
-    if (use_conv7() && phases == 1 && a.taps == 7 && a.a_stride == 1 && a.c_stride == 1 && a.c_off == 0 &&
-        a.a_off == -3 * a.dil && a.dil <= 9 && a.L_out == a.M && a.L_in == a.M && !a.res && !a.out && a.out_s) {
+    const bool k7 = phases == 1 && a.taps == 7 && a.a_stride == 1 && a.c_stride == 1 && a.c_off == 0 &&
+                    a.a_off == -3 * a.dil && a.dil <= 9 && a.L_out == a.M && a.L_in == a.M && !a.res && !a.out && a.out_s;
+    if (k7 && knobs().conv7 == 2 && a.in_halo && a.N % 256 == 0 && 3 * a.dil <= kActPadRows && a.M < (1ll << 31)) {
+        // the k = 7 conv as an implicit GEMM on the two-phase ping-pong tile (256 × 256, eight
+        // waves; gemm.hip EPI_SNAKE): its halo rows come from the buffer's zero rows — the front
+        // ones are never written, the back ones are cleared here
+        HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * a.Cin), 0, (size_t)3 * a.dil * a.Cin * 2, s));
+        GemmArgs g{};
+        g.A = a.in; g.lda = a.Cin;
+        g.W = a.W; g.ldw = 7 * a.Cin;
+        g.C = a.out_s; g.ldc = a.N;
+        g.M = (int)a.M; g.N = a.N; g.K = 7 * a.Cin;
+        g.epi = EPI_SNAKE; g.bias = a.bias; g.sa = a.sa; g.sib = a.sib;
+        g.conv_cin = a.Cin; g.conv_dil = a.dil;
+        return gemm_conv7(g, s);
+    }
+    if (use_conv7() && k7) {
         const int64_t t7 = ((a.M + CONV7_BM - 1) / CONV7_BM) * (a.N / 128);
         if (t7 >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");
         conv7_kernel<CONV7_BM, false, false><<<(unsigned)t7, CONV7_BM * 2, 0, s>>>(a, ResUnitArgs{});

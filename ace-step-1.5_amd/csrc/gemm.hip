@@ -154,7 +154,7 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
 #pragma unroll
                 for (int jp = 0; jp < NP; ++jp) {
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                    if constexpr (EPI == EPI_STORE) {
+                    if constexpr (EPI == EPI_STORE || EPI == EPI_SNAKE) {
                         if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n);
                     } else {
                         rv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
@@ -174,12 +174,24 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                     float o[8];
                     pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                    if constexpr (EPI == EPI_STORE) {
+                    if constexpr (EPI == EPI_STORE || EPI == EPI_SNAKE) {
                         if (a.bias) {
                             float bb[8];
                             unpack8(rv[ii][jp], bb);
 #pragma unroll
                             for (int r = 0; r < 8; ++r) o[r] += bb[r];
+                        }
+                        if constexpr (EPI == EPI_SNAKE) {
+                            // the conv output rounded to bf16, then its Snake (conv.hip conv7_kernel)
+                            rbf_n<8>(o);
+                            const float4 a0 = *(const float4 *)(a.sa + n), a1 = *(const float4 *)(a.sa + n + 4);
+                            const float4 b0 = *(const float4 *)(a.sib + n), b1 = *(const float4 *)(a.sib + n + 4);
+                            const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                            float t[8];
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) t[r] = o[r];
+                            snake_n<8>(t, av, bv, o);
                         }
                     } else {
                         float rr[8];
@@ -540,8 +552,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     }
     auto stageA = [&](int buf, int k0) {
         char *b = lds + buf * BUF;
+        int ko = k0;
+        if constexpr (EPI == EPI_SNAKE) {
+            // implicit-GEMM conv: K-tile k0 = tap·cin + c0 reads the input rows shifted by
+            // (tap − 3)·dil (zero halo rows around the activation)
+            const int cin = a.conv_cin, tap = k0 / cin;
+            ko = k0 + tap * (a.conv_dil - 1) * cin - 3 * a.conv_dil * cin;
+        }
 #pragma unroll
-        for (int i = 0; i < NA; ++i) glds16(srcA[i] + k0, b + (wave + 8 * i) * 1024);
+        for (int i = 0; i < NA; ++i) glds16(srcA[i] + ko, b + (wave + 8 * i) * 1024);
     };
     auto stageB = [&](int buf, int k0) {
         char *b = lds + buf * BUF + BM * 128;
@@ -878,6 +897,12 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
+        case EPI_SNAKE:
+            if constexpr (BM == 256) {
+                gemm_pp_kernel<BM, EPI_SNAKE><<<tiles, 512, 0, s>>>(a);
+                break;
+            }
+            return fail(-1, "gemm: the conv epilogue runs on the 256-row ping-pong tile");
         case EPI_HEADPOST:
             if constexpr (BM == 192 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
@@ -1097,6 +1122,15 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     // ACEHIP_GEMM_TAIL=1: the tail as one round of 128×256 two-phase ping-pong tiles
     const bool pp128 = knobs().gemm_tail == 1 && a.N % 256 == 0 && ((tl.M + 127) / 128) * nN <= cus;
     return gemm_variant(tl, pp128 ? 9 : 0, s);
+}
+
+int gemm_conv7(const GemmArgs &a, hipStream_t s) {
+    if (a.epi != EPI_SNAKE || !a.sa || !a.sib || a.conv_cin <= 0 || a.conv_dil < 1 || a.M <= 0)
+        return fail(-1, "gemm_conv7: EPI_SNAKE with snake parameters and conv geometry required");
+    if (a.N % 256 || a.conv_cin % BK || a.K != 7 * a.conv_cin || a.lda != a.conv_cin || a.ldw != a.K || a.ldc != a.N)
+        return fail(-1, "gemm_conv7: N % 256, cin % 64, K = 7·cin and dense layouts required");
+    if ((int64_t)((a.M + 255) / 256) * (a.N / 256) >= (1ll << 31)) return fail(-1, "gemm_conv7: grid too large");
+    return launch_pp<256>(a, s);
 }
 
 int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {

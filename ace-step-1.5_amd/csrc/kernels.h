@@ -25,7 +25,7 @@ struct Knobs {
     int fuse_rowadd = 1;      // ACEHIP_FUSE_ROWADD: null-row constant added in the MLP norm
     int dit_dedup = 1;        // ACEHIP_DIT_DEDUP: layer-0 CFG row dedup
     int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body
-    int conv7 = 1;            // ACEHIP_CONV7: halo-staged k = 7 VAE convs
+    int conv7 = 2;            // ACEHIP_CONV7: k = 7 VAE convs — 2 implicit GEMM on the ping-pong tile (C ≥ 256, padded input), 1 halo-staged conv7_kernel
     int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
     int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
     int vae_snake_in = 1;     // ACEHIP_VAE_SNAKE_IN: C = 128 decoder blocks without x_s tensors (ru8 SIN)
@@ -73,8 +73,14 @@ struct GemmArgs {
     // + a bf16 [M][N] staging tile for the head-post case; null disables split-K
     void *ws; size_t ws_bytes;
     int kper;                       // internal: K-tiles per split (EPI_PARTIAL launches)
+    // EPI_SNAKE (gemm_conv7 only): the k = 7 dilated conv as an implicit GEMM — A(m, k) =
+    // in[m + (k / conv_cin − 3)·conv_dil][k % conv_cin] (A = in, lda = conv_cin), W the packed
+    // [N][7·conv_cin] taps; C = bf16(snake(bf16(acc + bias))) with per-column sa / sib
+    const float *sa, *sib;
+    int conv_cin, conv_dil;
 };
 constexpr int EPI_PARTIAL = 5;                       // internal: fp32 partials of split blockIdx.y → ws
+constexpr int EPI_SNAKE = 6;                         // the VAE's k = 7 conv → Snake (gemm_conv7)
 constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace
 struct RowAdd;
 // defer != null: a residual-epilogue GEMM (EPI_GATED_RES / EPI_RES) that takes the small-M
@@ -82,6 +88,9 @@ struct RowAdd;
 // consumer rmsnorm_mod applies it, one launch fewer); defer->part stays null otherwise
 int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer = nullptr);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
+// the VAE's C ≥ 256 k = 7 convs on the two-phase ping-pong tile (EPI_SNAKE; the caller zeroes the
+// input's halo rows: ≥ 3·dil zero rows before row 0 and after row M − 1)
+int gemm_conv7(const GemmArgs &a, hipStream_t s);
 // Launch-attached timing events for the next GEMM of this thread (the SwiGLU paths: ping-pong,
 // generic and four-wave tiles): its first launch takes `start`, every launch `stop` (the last
 // completion wins), by hipExtLaunchKernel — no separate event packets in the stream.

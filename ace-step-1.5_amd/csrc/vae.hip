@@ -153,8 +153,9 @@ int make_res(acehip_vae *h, const std::string &p, int C, int dil, ResU &r) {
 // handles on different devices or threads never share launch state)
 int run_conv(const bf16_t *zero, const ConvL &c, const bf16_t *in, int64_t L_in, int64_t M, int taps, int dil, int a_stride,
              int a_off, int c_stride, int c_off, int64_t L_out, bf16_t *out, bf16_t *out_s, const SnakeP *sn,
-             const bf16_t *res, int phases, hipStream_t s) {
+             const bf16_t *res, int phases, hipStream_t s, int in_halo = 0) {
     ConvArgs a{};
+    a.in_halo = in_halo;
     a.in = in; a.L_in = L_in; a.Cin = c.cin;
     a.W = c.Wp; a.w_pstride = (int64_t)c.cout * taps * c.cin;
     a.bias = c.bias; a.out = out; a.out_s = out_s;
@@ -184,7 +185,8 @@ int res_unit(const bf16_t *zero, const ResU &r, int64_t L, bf16_t *X, bf16_t *cu
         // the snaked output is in `other`: copy-free hand-back by swapping roles is done by the caller
         return 1;   // signals "output in other"
     }
-    if ((rc = run_conv(zero, r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s)))
+    // (cur is one of the padded activation buffers: in_halo)
+    if ((rc = run_conv(zero, r.c1, cur, L, L, 7, r.dil, 1, -3 * r.dil, 1, 0, L, nullptr, other, &r.s2, nullptr, 1, s, 1)))
         return rc;
     return run_conv(zero, r.c2, other, L, L, 1, 1, 1, 0, 1, 0, L, keep_raw ? X : nullptr, cur, &next, X, 1, s);
 }
@@ -589,7 +591,19 @@ int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void 
     bf16_t *o = (bf16_t *)out, *os = (bf16_t *)out_s;
     const bf16_t *x = (const bf16_t *)in, *r = (const bf16_t *)res;
     const int pad = (stride + 1) / 2;
-    if (kind == 0) rc = run_conv(zero, c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s);
+    int halo = 0;
+    if (kind == 0 && k == 7 && knobs().conv7 == 2) {
+        // stage the input the way the decoder's activation buffers hold it (zero rows around
+        // it), so the unit test exercises the implicit-GEMM k = 7 path (ACEHIP_CONV7=2)
+        const size_t rowb = (size_t)Cin * 2, padb = (size_t)kActPadRows * rowb;
+        char *xp = (char *)t.get((size_t)L_in * rowb + 2 * padb);
+        if (!xp) return fail(ACEHIP_E_OOM, "vae_conv: oom");
+        HIP_TRY(hipMemsetAsync(xp, 0, padb, s));
+        HIP_TRY(hipMemcpyAsync(xp + padb, in, (size_t)L_in * rowb, hipMemcpyDeviceToDevice, s));
+        x = (const bf16_t *)(xp + padb);
+        halo = 1;
+    }
+    if (kind == 0) rc = run_conv(zero, c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s, halo);
     else if (kind == 1)
         rc = run_conv(zero, c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s);
     else rc = run_conv(zero, c, x, L_in, L_in / stride, k, 1, stride, -pad, 1, 0, L_in / stride, o, os, snp, r, 1, s);

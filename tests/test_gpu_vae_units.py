@@ -103,6 +103,30 @@ def test_vae_conv_unit(gpu_device, kind, Cin, Cout, k, stride, dil, L, raw, use_
         assert rel_l2(out_s, ys) < TOL, ("snake", rel_l2(out_s, ys))
 
 
+@pytest.mark.parametrize("Cin,Cout,dil,L", [(256, 256, 1, 1000), (256, 256, 9, 1000), (512, 512, 3, 700),
+                                          (1024, 1024, 3, 300), (1024, 1024, 9, 257), (512, 256, 1, 33)])
+def test_vae_conv7_implicit_gemm(gpu_device, monkeypatch, Cin, Cout, dil, L):
+    """ACEHIP_CONV7=2: the C ≥ 256 k = 7 convs as an implicit GEMM on the two-phase ping-pong
+    tile (gemm.hip EPI_SNAKE; halo rows read from the zero rows around the activation) against
+    the fp32 torch conv + Snake, and against the halo-staged conv7_kernel (both round the conv
+    output to bf16 once before the Snake; only their fp32 accumulation orders differ).  L = 257
+    and 33: partial last 256-row tiles; dil 9: the widest halo (27 rows each side)."""
+    g = torch.Generator(device=gpu_device).manual_seed(Cin + Cout + dil + L)
+    x = _bf(torch.randn(L, Cin, device=gpu_device, generator=g))
+    w = _bf(torch.randn(Cout, Cin, 7, device=gpu_device, generator=g) / math.sqrt(Cin * 7))
+    bias = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.1)
+    alpha = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.3)
+    beta = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.3)
+    set_knob(monkeypatch, "ACEHIP_CONV7", "2")
+    _, gemm_s = _run_conv(0, x, w, bias, None, Cout, 7, 1, dil, False, alpha, beta)
+    set_knob(monkeypatch, "ACEHIP_CONV7", "1")
+    _, halo_s = _run_conv(0, x, w, bias, None, Cout, 7, 1, dil, False, alpha, beta)
+    torch.cuda.synchronize()
+    ys = snake(_ref_conv(0, x, w, bias, 7, 1, dil), alpha, beta)
+    assert rel_l2(gemm_s, ys) < TOL, rel_l2(gemm_s, ys)
+    assert rel_l2(gemm_s, halo_s) < 4e-3, rel_l2(gemm_s, halo_s)
+
+
 def _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep):
     C = x.shape[1]
     x_out = torch.empty(L, C, device=x.device, dtype=torch.bfloat16) if keep else None
