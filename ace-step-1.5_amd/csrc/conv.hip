@@ -1956,17 +1956,35 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
                     a.a_off == -3 * a.dil && a.dil <= 9 && a.L_out == a.M && a.L_in == a.M && !a.res && !a.out && a.out_s;
     if (k7 && knobs().conv7 == 2 && a.in_halo && a.N % 256 == 0 && 3 * a.dil <= kActPadRows && a.M < (1ll << 31)) {
         // the k = 7 conv as an implicit GEMM on the two-phase ping-pong tile (256 × 256, eight
-        // waves; gemm.hip EPI_SNAKE): its halo rows come from the buffer's zero rows — the front
+        // waves; gemm.hip EPI_CONV): its halo rows come from the buffer's zero rows — the front
         // ones are never written, the back ones are cleared here
         HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * a.Cin), 0, (size_t)3 * a.dil * a.Cin * 2, s));
         GemmArgs g{};
         g.A = a.in; g.lda = a.Cin;
         g.W = a.W; g.ldw = 7 * a.Cin;
-        g.C = a.out_s; g.ldc = a.N;
+        g.Cs = a.out_s; g.ldc = a.N;
         g.M = (int)a.M; g.N = a.N; g.K = 7 * a.Cin;
-        g.epi = EPI_SNAKE; g.bias = a.bias; g.sa = a.sa; g.sib = a.sib;
-        g.conv_cin = a.Cin; g.conv_dil = a.dil;
-        return gemm_conv7(g, s);
+        g.epi = EPI_CONV; g.bias = a.bias; g.sa = a.sa; g.sib = a.sib;
+        g.conv_cin = a.Cin; g.conv_dil = a.dil; g.conv_a0 = -3 * a.dil;
+        g.conv_ostride = 1; g.conv_ooff = 0; g.conv_cout = a.N; g.conv_lout = a.L_out;
+        return gemm_conv(g, s);
+    }
+    // ConvTranspose1d (stride s, kernel 2s): the s phases' two-tap GEMMs side by side along N
+    // (N = s·Cout, A — input rows m − 1 and m — read once for all of them), column n → channel
+    // n % Cout of phase n / Cout at output row m·s − pad + phase; the same padded input
+    if (knobs().convt && a.in_halo && phases > 1 && a.taps == 2 && a.a_stride == 1 && a.a_off == -1 && a.dil == 1 &&
+        a.c_stride == phases && a.M == a.L_in + 1 && !a.res && (int64_t)phases * a.N % 256 == 0 &&
+        a.w_pstride == (int64_t)a.N * 2 * a.Cin && a.M < (1ll << 31)) {
+        HIP_TRY(hipMemsetAsync((void *)(a.in + a.L_in * a.Cin), 0, (size_t)a.Cin * 2, s));
+        GemmArgs g{};
+        g.A = a.in; g.lda = a.Cin;
+        g.W = a.W; g.ldw = 2 * a.Cin;
+        g.C = a.out; g.Cs = a.out_s; g.ldc = a.N;
+        g.M = (int)a.M; g.N = phases * a.N; g.K = 2 * a.Cin;
+        g.epi = EPI_CONV; g.bias = a.bias; g.sa = a.sa; g.sib = a.sib;
+        g.conv_cin = a.Cin; g.conv_dil = 1; g.conv_a0 = -1;
+        g.conv_ostride = phases; g.conv_ooff = a.c_off; g.conv_cout = a.N; g.conv_lout = a.L_out;
+        return gemm_conv(g, s);
     }
     if (use_conv7() && k7) {
         const int64_t t7 = ((a.M + CONV7_BM - 1) / CONV7_BM) * (a.N / 128);

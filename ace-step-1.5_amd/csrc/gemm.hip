@@ -154,8 +154,10 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
 #pragma unroll
                 for (int jp = 0; jp < NP; ++jp) {
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                    if constexpr (EPI == EPI_STORE || EPI == EPI_SNAKE) {
+                    if constexpr (EPI == EPI_STORE) {
                         if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n);
+                    } else if constexpr (EPI == EPI_CONV) {
+                        if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n % a.conv_cout);
                     } else {
                         rv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
                         if constexpr (EPI == EPI_GATED_RES)
@@ -174,24 +176,30 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                     float o[8];
                     pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                    if constexpr (EPI == EPI_STORE || EPI == EPI_SNAKE) {
+                    if constexpr (EPI == EPI_STORE || EPI == EPI_CONV) {
                         if (a.bias) {
                             float bb[8];
                             unpack8(rv[ii][jp], bb);
 #pragma unroll
                             for (int r = 0; r < 8; ++r) o[r] += bb[r];
                         }
-                        if constexpr (EPI == EPI_SNAKE) {
-                            // the conv output rounded to bf16, then its Snake (conv.hip conv7_kernel)
+                        if constexpr (EPI == EPI_CONV) {
+                            // the conv output rounded to bf16 (raw), then its Snake (conv.hip)
                             rbf_n<8>(o);
-                            const float4 a0 = *(const float4 *)(a.sa + n), a1 = *(const float4 *)(a.sa + n + 4);
-                            const float4 b0 = *(const float4 *)(a.sib + n), b1 = *(const float4 *)(a.sib + n + 4);
-                            const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-                            float t[8];
-#pragma unroll
-                            for (int r = 0; r < 8; ++r) t[r] = o[r];
-                            snake_n<8>(t, av, bv, o);
+                            const int ph = n / a.conv_cout, col = n - ph * a.conv_cout;
+                            const int64_t orow = (int64_t)m * a.conv_ostride + a.conv_ooff + ph;
+                            const bool ok = live && orow >= 0 && orow < a.conv_lout;
+                            if (a.C && ok) *(uint4 *)(a.C + orow * a.ldc + col) = pack8(o);
+                            if (a.Cs) {
+                                const float4 a0 = *(const float4 *)(a.sa + col), a1 = *(const float4 *)(a.sa + col + 4);
+                                const float4 b0 = *(const float4 *)(a.sib + col), b1 = *(const float4 *)(a.sib + col + 4);
+                                const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                                const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                                float sn[8];
+                                snake_n<8>(o, av, bv, sn);
+                                if (ok) *(uint4 *)(a.Cs + orow * a.ldc + col) = pack8(sn);
+                            }
+                            continue;
                         }
                     } else {
                         float rr[8];
@@ -553,11 +561,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     auto stageA = [&](int buf, int k0) {
         char *b = lds + buf * BUF;
         int ko = k0;
-        if constexpr (EPI == EPI_SNAKE) {
+        if constexpr (EPI == EPI_CONV) {
             // implicit-GEMM conv: K-tile k0 = tap·cin + c0 reads the input rows shifted by
-            // (tap − 3)·dil (zero halo rows around the activation)
+            // conv_a0 + tap·dil (zero halo rows around the activation)
             const int cin = a.conv_cin, tap = k0 / cin;
-            ko = k0 + tap * (a.conv_dil - 1) * cin - 3 * a.conv_dil * cin;
+            ko = k0 + tap * (a.conv_dil - 1) * cin + a.conv_a0 * cin;
         }
 #pragma unroll
         for (int i = 0; i < NA; ++i) glds16(srcA[i] + ko, b + (wave + 8 * i) * 1024);
@@ -897,9 +905,9 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_GATED_RES: gemm_pp_kernel<BM, EPI_GATED_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
-        case EPI_SNAKE:
+        case EPI_CONV:
             if constexpr (BM == 256) {
-                gemm_pp_kernel<BM, EPI_SNAKE><<<tiles, 512, 0, s>>>(a);
+                gemm_pp_kernel<BM, EPI_CONV><<<tiles, 512, 0, s>>>(a);
                 break;
             }
             return fail(-1, "gemm: the conv epilogue runs on the 256-row ping-pong tile");
@@ -1124,12 +1132,13 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     return gemm_variant(tl, pp128 ? 9 : 0, s);
 }
 
-int gemm_conv7(const GemmArgs &a, hipStream_t s) {
-    if (a.epi != EPI_SNAKE || !a.sa || !a.sib || a.conv_cin <= 0 || a.conv_dil < 1 || a.M <= 0)
-        return fail(-1, "gemm_conv7: EPI_SNAKE with snake parameters and conv geometry required");
-    if (a.N % 256 || a.conv_cin % BK || a.K != 7 * a.conv_cin || a.lda != a.conv_cin || a.ldw != a.K || a.ldc != a.N)
-        return fail(-1, "gemm_conv7: N % 256, cin % 64, K = 7·cin and dense layouts required");
-    if ((int64_t)((a.M + 255) / 256) * (a.N / 256) >= (1ll << 31)) return fail(-1, "gemm_conv7: grid too large");
+int gemm_conv(const GemmArgs &a, hipStream_t s) {
+    if (a.epi != EPI_CONV || (!a.C && !a.Cs) || (a.Cs && (!a.sa || !a.sib)) || a.conv_cin <= 0 || a.conv_dil < 1 ||
+        a.conv_ostride < 1 || a.conv_cout <= 0 || a.conv_cout % 8 || a.N % a.conv_cout || a.conv_lout <= 0 || a.M <= 0)
+        return fail(-1, "gemm_conv: EPI_CONV with an output, snake parameters and conv geometry required");
+    if (a.N % 256 || a.conv_cin % BK || a.K % a.conv_cin || a.lda != a.conv_cin || a.ldw != a.K || a.ldc != a.conv_cout)
+        return fail(-1, "gemm_conv: N % 256, cin % 64, K = taps·cin and dense layouts required");
+    if ((int64_t)((a.M + 255) / 256) * (a.N / 256) >= (1ll << 31)) return fail(-1, "gemm_conv: grid too large");
     return launch_pp<256>(a, s);
 }
 

@@ -25,6 +25,7 @@ struct Knobs {
     int fuse_rowadd = 1;      // ACEHIP_FUSE_ROWADD: null-row constant added in the MLP norm
     int dit_dedup = 1;        // ACEHIP_DIT_DEDUP: layer-0 CFG row dedup
     int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body
+    int convt = 1;            // ACEHIP_CONVT: 1 ConvTranspose (N % 256 == 0, padded input) as an implicit GEMM, 0 conv_gemm_kernel
     int conv7 = 2;            // ACEHIP_CONV7: k = 7 VAE convs — 2 implicit GEMM on the ping-pong tile (C ≥ 256, padded input), 1 halo-staged conv7_kernel
     int convp = 2;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel
     int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
@@ -73,14 +74,20 @@ struct GemmArgs {
     // + a bf16 [M][N] staging tile for the head-post case; null disables split-K
     void *ws; size_t ws_bytes;
     int kper;                       // internal: K-tiles per split (EPI_PARTIAL launches)
-    // EPI_SNAKE (gemm_conv7 only): the k = 7 dilated conv as an implicit GEMM — A(m, k) =
-    // in[m + (k / conv_cin − 3)·conv_dil][k % conv_cin] (A = in, lda = conv_cin), W the packed
-    // [N][7·conv_cin] taps; C = bf16(snake(bf16(acc + bias))) with per-column sa / sib
+    // EPI_CONV (gemm_conv only): a VAE convolution as an implicit GEMM.  Tap t = k / conv_cin
+    // reads A(m, k) = in[m + conv_a0 + t·conv_dil][k % conv_cin] (A = in, lda = conv_cin; the
+    // caller provides zero rows around the input).  Column n is output channel n % conv_cout of
+    // phase p = n / conv_cout (a ConvTranspose's phases side by side: W = the packed
+    // [phases][conv_cout][taps·cin] taps); row m lands on output row m·conv_ostride + conv_ooff + p
+    // when that lies in [0, conv_lout): raw bf16(acc + bias) to C (if set), its Snake (sa / sib)
+    // to Cs (if set), both with row pitch ldc = conv_cout
     const float *sa, *sib;
-    int conv_cin, conv_dil;
+    bf16_t *Cs;
+    int conv_cin, conv_dil, conv_a0, conv_ostride, conv_ooff, conv_cout;
+    int64_t conv_lout;
 };
 constexpr int EPI_PARTIAL = 5;                       // internal: fp32 partials of split blockIdx.y → ws
-constexpr int EPI_SNAKE = 6;                         // the VAE's k = 7 conv → Snake (gemm_conv7)
+constexpr int EPI_CONV = 6;                          // the VAE's implicit-GEMM convs (gemm_conv)
 constexpr size_t GEMM_WS_BYTES = (size_t)48 << 20;   // runtimes' split-K workspace
 struct RowAdd;
 // defer != null: a residual-epilogue GEMM (EPI_GATED_RES / EPI_RES) that takes the small-M
@@ -88,9 +95,9 @@ struct RowAdd;
 // consumer rmsnorm_mod applies it, one launch fewer); defer->part stays null otherwise
 int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer = nullptr);
 int gemm_variant(const GemmArgs &a, int variant, hipStream_t s);   // tuning / tests
-// the VAE's C ≥ 256 k = 7 convs on the two-phase ping-pong tile (EPI_SNAKE; the caller zeroes the
-// input's halo rows: ≥ 3·dil zero rows before row 0 and after row M − 1)
-int gemm_conv7(const GemmArgs &a, hipStream_t s);
+// VAE convolutions (k = 7 dilated, ConvTranspose phases) on the two-phase ping-pong tile
+// (EPI_CONV; the caller provides the input's zero halo rows)
+int gemm_conv(const GemmArgs &a, hipStream_t s);
 // Launch-attached timing events for the next GEMM of this thread (the SwiGLU paths: ping-pong,
 // generic and four-wave tiles): its first launch takes `start`, every launch `stop` (the last
 // completion wins), by hipExtLaunchKernel — no separate event packets in the stream.

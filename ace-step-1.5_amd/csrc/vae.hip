@@ -207,7 +207,7 @@ int dec_block_snake_in(acehip_vae *h, int j, int64_t &L, bf16_t *&X, bf16_t *&cu
     int rc;
     // ConvTranspose1d → raw x only
     if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, nullptr, nullptr, nullptr,
-                       st, s)))
+                       st, s, 1)))
         return rc;
     L *= st;
     bf16_t *bufs[3] = {X, cur, other};          // raw x in bufs[0]; unit u: in bufs[u] → out bufs[u + 1 mod 3]
@@ -434,7 +434,7 @@ int acehip_vae_decode(acehip_vae *h, const void *z, int B, int T, void *wav, voi
             }
             // ConvTranspose1d as `st` phase GEMMs → raw x (residual) + snaked x for res_unit1
             if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
-                               nullptr, st, s)))
+                               nullptr, st, s, 1)))
                 return rc;
             L *= st;
             std::swap(cur, other);
@@ -474,7 +474,7 @@ int acehip_vae_decode_blocks(acehip_vae *h, const void *z, int T, int n_blocks, 
             continue;
         }
         if ((rc = run_conv(h->zero, bk.convT, cur, L, L + 1, 2, 1, 1, -1, st, -pad, L * st, X, other, &bk.res[0].s1,
-                           nullptr, st, s)))
+                           nullptr, st, s, 1)))
             return rc;
         L *= st;
         C = bk.cout;
@@ -592,9 +592,9 @@ int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void 
     const bf16_t *x = (const bf16_t *)in, *r = (const bf16_t *)res;
     const int pad = (stride + 1) / 2;
     int halo = 0;
-    if (kind == 0 && k == 7 && knobs().conv7 == 2) {
+    if ((kind == 0 && k == 7 && knobs().conv7 == 2) || (kind == 1 && knobs().convt)) {
         // stage the input the way the decoder's activation buffers hold it (zero rows around
-        // it), so the unit test exercises the implicit-GEMM k = 7 path (ACEHIP_CONV7=2)
+        // it), so the unit test exercises the implicit-GEMM paths (ACEHIP_CONV7=2, ACEHIP_CONVT=1)
         const size_t rowb = (size_t)Cin * 2, padb = (size_t)kActPadRows * rowb;
         char *xp = (char *)t.get((size_t)L_in * rowb + 2 * padb);
         if (!xp) return fail(ACEHIP_E_OOM, "vae_conv: oom");
@@ -605,7 +605,7 @@ int acehip_vae_conv(int kind, const void *in, int64_t L_in, int Cin, const void 
     }
     if (kind == 0) rc = run_conv(zero, c, x, L_in, L_in, k, dil, 1, -dil * (k - 1) / 2, 1, 0, L_in, o, os, snp, r, 1, s, halo);
     else if (kind == 1)
-        rc = run_conv(zero, c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s);
+        rc = run_conv(zero, c, x, L_in, L_in + 1, 2, 1, 1, -1, stride, -pad, L_in * stride, o, os, snp, r, stride, s, halo);
     else rc = run_conv(zero, c, x, L_in, L_in / stride, k, 1, stride, -pad, 1, 0, L_in / stride, o, os, snp, r, 1, s);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));

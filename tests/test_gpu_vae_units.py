@@ -127,6 +127,38 @@ def test_vae_conv7_implicit_gemm(gpu_device, monkeypatch, Cin, Cout, dil, L):
     assert rel_l2(gemm_s, halo_s) < 4e-3, rel_l2(gemm_s, halo_s)
 
 
+@pytest.mark.parametrize("Cin,Cout,stride,L,raw,use_snake", [(2048, 1024, 10, 40, True, True), (1024, 512, 6, 96, True, True),
+                                                            (512, 256, 4, 300, True, True), (512, 256, 4, 257, False, True),
+                                                            (1024, 512, 6, 1, True, False), (256, 128, 4, 700, True, False),
+                                                            (128, 128, 2, 1500, True, True), (128, 128, 2, 3, True, True)])
+def test_vae_convt_implicit_gemm(gpu_device, monkeypatch, Cin, Cout, stride, L, raw, use_snake):
+    """ACEHIP_CONVT=1: ConvTranspose1d (kernel 2s, stride s, padding ⌈s/2⌉) as the s phases'
+    two-tap GEMMs side by side along N on the ping-pong tile (column n → channel n % Cout of
+    phase n / Cout, output row m·s − pad + phase, rows outside [0, L·s) dropped; the C = 128
+    blocks' Cout = 128 included) against torch's conv_transpose1d (+ Snake) and against the
+    conv_gemm_kernel path (ACEHIP_CONVT=0).  L = 1: a single input row (every output row comes
+    from the zero halo rows on one side)."""
+    g = torch.Generator(device=gpu_device).manual_seed(Cin + Cout + stride + L)
+    x = _bf(torch.randn(L, Cin, device=gpu_device, generator=g))
+    w = _bf(torch.randn(Cin, Cout, 2 * stride, device=gpu_device, generator=g) / math.sqrt(Cin * 2))
+    bias = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.1)
+    alpha = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.3) if use_snake else None
+    beta = _bf(torch.randn(Cout, device=gpu_device, generator=g) * 0.3) if use_snake else None
+    set_knob(monkeypatch, "ACEHIP_CONVT", "1")
+    out, out_s = _run_conv(1, x, w, bias, None, Cout, 2 * stride, stride, 1, raw, alpha, beta)
+    set_knob(monkeypatch, "ACEHIP_CONVT", "0")
+    out0, out_s0 = _run_conv(1, x, w, bias, None, Cout, 2 * stride, stride, 1, raw, alpha, beta)
+    torch.cuda.synchronize()
+    y = _ref_conv(1, x, w, bias, 2 * stride, stride, 1)
+    if raw:
+        assert rel_l2(out, y) < TOL, rel_l2(out, y)
+        assert rel_l2(out, out0) < 4e-3, rel_l2(out, out0)
+    if use_snake:
+        ys = snake(y, alpha, beta)
+        assert rel_l2(out_s, ys) < TOL, rel_l2(out_s, ys)
+        assert rel_l2(out_s, out_s0) < 4e-3, rel_l2(out_s, out_s0)
+
+
 def _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep):
     C = x.shape[1]
     x_out = torch.empty(L, C, device=x.device, dtype=torch.bfloat16) if keep else None
