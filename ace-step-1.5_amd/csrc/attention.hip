@@ -265,9 +265,14 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     // (whole units only: the tail-split parts must stay the grid's last blocks)
     const bool streamk = sp.sk_total > 0;
     int64_t g0 = 0, g1 = 0;                 // stream-K: this workgroup's global tile range
+    // stream-K logical workgroup: the blocks of one XCD (bid ≡ x mod 8) take a contiguous range
+    // of the tile sequence, so the units they walk share few K/V heads in that XCD's L2 (with
+    // blockIdx.x itself, neighbouring ranges went to different XCDs: L2 hit rate 48 %,
+    // profiles/r05v_pmc_tcc.json); slabs and flags are indexed by the logical number
+    const int cw = (streamk && ATT_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (streamk) {
-        g0 = (int64_t)blockIdx.x * sp.sk_total / gridDim.x;
-        g1 = ((int64_t)blockIdx.x + 1) * sp.sk_total / gridDim.x;
+        g0 = (int64_t)cw * sp.sk_total / gridDim.x;
+        g1 = ((int64_t)cw + 1) * sp.sk_total / gridDim.x;
         if (g0 >= g1) return;
     }
     for (;;) {                              // pieces (one unless stream-K)
@@ -613,16 +618,16 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         const int64_t wsz = 66 * 64;                   // floats per wave: 64 O + m + l per lane
         if (pt0 > 0) {
             // a later piece of unit u (this workgroup's first piece): publish slab c, then the flag
-            slab_store(sp.ws + ((int64_t)blockIdx.x * 8 + wave) * wsz, oacc, m, l, lane);
+            slab_store(sp.ws + ((int64_t)cw * 8 + wave) * wsz, oacc, m, l, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(sp.flags + blockIdx.x, sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) __hip_atomic_store(sp.flags + cw, sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             write_o = false;
         } else {
             // the piece with tile 0 (this workgroup's last): fold the later pieces in order — the
             // first pieces of workgroups c+1, c+2, … that start inside unit u
             const int64_t uend = ((int64_t)u + 1) * sp.sk_nt;
-            for (int c2 = blockIdx.x + 1; c2 < (int)gridDim.x; ++c2) {
+            for (int c2 = cw + 1; c2 < (int)gridDim.x; ++c2) {
                 if ((int64_t)c2 * sp.sk_total / gridDim.x >= uend) break;
                 __shared__ int s_ok;
                 if (tid == 0) {

@@ -127,7 +127,7 @@ def main():
           "clock_GHz": round(clk, 3) if clk and clk <= 2.4 else None,
           "per_kind": per_kind}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES,GRBM_GUI_ACTIVE,"
-                     "SQ_BUSY_CYCLES, each its own --kernel-trace pass over tools/prof_dit.py --forwards 1",
+                     "SQ_BUSY_CYCLES, each its own --kernel-trace pass over tools/prof_dit.py (--forwards from the --calls count: 24 SwiGLU calls per forward)",
            "box": a.box, "git_head": a.git, "product_hash": _product_hash(),
            "note": "separate counter passes (not the bench's timed run); profiled passes run at a lower "
                    "clock than un-profiled ones (guide 'DVFS give-back' (2)); clock_GHz is withheld when "
