@@ -14,7 +14,10 @@ hash) and gpurun_out/<tag>_pmc_tcc.json (per kernel: TCC hits, misses, hit rate 
 misses) — MI355X_MICROARCH.md §L2 — and the L2-miss bytes at 128 B per miss), then deletes the
 trace databases (gpurun_out is merged back only up to 64 MiB).
 
-usage: pmc_final.py TAG"""
+With MODE "vae": only the FETCH_SIZE and WRITE_SIZE passes, over tools/prof_dit.py --forwards 0
+--vae (one 240 s decode), summarised by tools/pmc_vae.py → gpurun_out/<tag>_pmc_vae_traffic.json.
+
+usage: pmc_final.py TAG [vae]"""
 import glob
 import json
 import os
@@ -28,11 +31,11 @@ PASSES = [("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"),
           ("sq", "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"), ("tcc", "TCC_HIT_sum TCC_MISS_sum")]
 
 
-def run_pass(tag, name, counters):
+def run_pass(tag, name, counters, driver=("--forwards", "2")):
     d = os.path.join(REPO, "gpurun_out", f"{tag}_pmc_{name}")
     shutil.rmtree(d, ignore_errors=True)
     cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *counters.split(), "--kernel-trace", "-d", d, "-o",
-           "run", "--", "python3", os.path.join(REPO, "tools", "prof_dit.py"), "--forwards", "2"]
+           "run", "--", "python3", os.path.join(REPO, "tools", "prof_dit.py"), *driver]
     print("==", " ".join(cmd), flush=True)
     with open(d + ".log", "w") as log:
         rc = subprocess.run(cmd, stdout=log, stderr=subprocess.STDOUT, cwd=REPO).returncode
@@ -46,8 +49,23 @@ def run_pass(tag, name, counters):
     return d, dbs[0]
 
 
+def main_vae(tag):
+    dirs, dbs = [], {}
+    for name, ctrs in PASSES[:2]:
+        d, db = run_pass(tag, "vae_" + name, ctrs, driver=("--forwards", "0", "--vae"))
+        dirs.append(d)
+        dbs[name] = db
+    rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_vae.py"), dbs["fetch"], dbs["write"],
+                         os.path.join(REPO, "gpurun_out", f"{tag}_pmc_vae_traffic.json")]).returncode
+    for d in dirs:
+        shutil.rmtree(d, ignore_errors=True)
+    sys.exit(rc)
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
+    if len(sys.argv) > 2 and sys.argv[2] == "vae":
+        main_vae(tag)
     dirs, dbs = [], {}
     for name, ctrs in PASSES:
         d, db = run_pass(tag, name, ctrs)

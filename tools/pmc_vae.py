@@ -42,7 +42,7 @@ def per_family(db, counter):
     return tot, {k: len(v) for k, v in n.items()}
 
 
-def algorithmic(T, snake_in=True):
+def algorithmic(T, snake_in=True, gemm_convs=True):
     """snake_in (ACEHIP_VAE_SNAKE_IN=1, the default since round 5): the C = 128 blocks keep no x_s
     tensor — their ConvTranspose writes raw x only and each residual unit reads x once and writes
     one output (raw x' for units 0, 1; the next block's snaked input for unit 2)."""
@@ -52,11 +52,15 @@ def algorithmic(T, snake_in=True):
     blocks = c.decoder_block_channels()
     c0 = blocks[0][0]
     fam["conv7_kernel"] += T * c.decoder_input_channels * B + T * c0 * B + 7 * c.decoder_input_channels * c0 * B
+    # gemm_convs (ACEHIP_CONV7=2, ACEHIP_CONVT=1, round 5): the ConvTransposes and the C ≥ 256 k7
+    # convs run on gemm_pp_kernel (EPI_CONV)
+    kt = "gemm_pp_kernel" if gemm_convs else "conv_gemm_kernel"
+    k7 = "gemm_pp_kernel" if gemm_convs else "conv7_kernel"
     L = T
     for cin, cout, s in blocks:
         Lo = L * s
         sin = snake_in and cout == 128
-        fam["conv_gemm_kernel"] += L * cin * B + (1 if sin else 2) * Lo * cout * B + cin * cout * 2 * s * B
+        fam[kt] += L * cin * B + (1 if sin else 2) * Lo * cout * B + cin * cout * 2 * s * B
         L = Lo
         for u in range(3):
             keep = u < 2
@@ -65,7 +69,7 @@ def algorithmic(T, snake_in=True):
             elif cout == 128:
                 fam["ru8_kernel"] += (2 + (2 if keep else 1)) * L * cout * B + 8 * cout * cout * B
             else:
-                fam["conv7_kernel"] += 2 * L * cout * B + 7 * cout * cout * B
+                fam[k7] += 2 * L * cout * B + 7 * cout * cout * B
                 fam["convp_kernel"] += (2 + (2 if keep else 1)) * L * cout * B + cout * cout * B
     fam["conv_out_kernel"] += L * 128 * B + L * 2 * 4
     return fam
@@ -78,10 +82,11 @@ def main():
     p.add_argument("out_json")
     p.add_argument("--T", type=int, default=6000)
     p.add_argument("--no-snake-in", action="store_true", help="model of ACEHIP_VAE_SNAKE_IN=0")
+    p.add_argument("--no-gemm-convs", action="store_true", help="model of ACEHIP_CONV7=1 ACEHIP_CONVT=0")
     a = p.parse_args()
     F, nF = per_family(a.fetch_db, "FETCH_SIZE")
     W, nW = per_family(a.write_db, "WRITE_SIZE")
-    alg = algorithmic(a.T, snake_in=not a.no_snake_in)
+    alg = algorithmic(a.T, snake_in=not a.no_snake_in, gemm_convs=not a.no_gemm_convs)
     out = {"T": a.T, "note": __doc__.split("\n\n")[0], "families": {}}
     tot_m = tot_a = 0.0
     for f in sorted(alg):
