@@ -1986,6 +1986,21 @@ int conv_gemm(const ConvArgs &a, int phases, hipStream_t s) {
         g.conv_ostride = phases; g.conv_ooff = a.c_off; g.conv_cout = a.N; g.conv_lout = a.L_out;
         return gemm_conv(g, s);
     }
+    // k = 1 convs (the C ≥ 256 residual units' second conv, with the residual) as a plain GEMM on
+    // the ping-pong tile (ACEHIP_CONVP=3)
+    if (knobs().convp == 3 && phases == 1 && a.taps == 1 && a.a_stride == 1 && a.a_off == 0 && a.c_stride == 1 &&
+        a.c_off == 0 && a.L_in == a.M && a.L_out == a.M && a.N % 256 == 0 && a.M < (1ll << 31)) {
+        GemmArgs g{};
+        g.A = a.in; g.lda = a.Cin;
+        g.W = a.W; g.ldw = a.Cin;
+        g.C = a.out; g.Cs = a.out_s; g.ldc = a.N;
+        g.res = a.res; g.ldr = a.N;
+        g.M = (int)a.M; g.N = a.N; g.K = a.Cin;
+        g.epi = EPI_CONV; g.bias = a.bias; g.sa = a.sa; g.sib = a.sib;
+        g.conv_cin = a.Cin; g.conv_dil = 1; g.conv_a0 = 0;
+        g.conv_ostride = 1; g.conv_ooff = 0; g.conv_cout = a.N; g.conv_lout = a.L_out;
+        return gemm_conv(g, s);
+    }
     if (use_conv7() && k7) {
         const int64_t t7 = ((a.M + CONV7_BM - 1) / CONV7_BM) * (a.N / 128);
         if (t7 >= (1ll << 31)) return fail(-1, "conv_gemm: grid too large");

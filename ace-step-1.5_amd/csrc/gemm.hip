@@ -158,6 +158,9 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                         if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n);
                     } else if constexpr (EPI == EPI_CONV) {
                         if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n % a.conv_cout);
+                        // residual (k = 1 convs of the C ≥ 256 residual units; one phase, so the
+                        // output row is m): loaded with the chunk, before any store — res may be C
+                        if (a.res) gv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
                     } else {
                         rv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
                         if constexpr (EPI == EPI_GATED_RES)
@@ -186,6 +189,13 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                         if constexpr (EPI == EPI_CONV) {
                             // the conv output rounded to bf16 (raw), then its Snake (conv.hip)
                             rbf_n<8>(o);
+                            if (a.res) {                     // x' = bf16(x + bf16(acc + b))
+                                float rr[8];
+                                unpack8(gv[ii][jp], rr);
+#pragma unroll
+                                for (int r = 0; r < 8; ++r) o[r] = rr[r] + o[r];
+                                rbf_n<8>(o);
+                            }
                             const int ph = n / a.conv_cout, col = n - ph * a.conv_cout;
                             const int64_t orow = (int64_t)m * a.conv_ostride + a.conv_ooff + ph;
                             const bool ok = live && orow >= 0 && orow < a.conv_lout;
@@ -1138,6 +1148,8 @@ int gemm_conv(const GemmArgs &a, hipStream_t s) {
         return fail(-1, "gemm_conv: EPI_CONV with an output, snake parameters and conv geometry required");
     if (a.N % 256 || a.conv_cin % BK || a.K % a.conv_cin || a.lda != a.conv_cin || a.ldw != a.K || a.ldc != a.conv_cout)
         return fail(-1, "gemm_conv: N % 256, cin % 64, K = taps·cin and dense layouts required");
+    if (a.res && (a.N != a.conv_cout || a.ldr != a.N || a.conv_ostride != 1 || a.conv_ooff != 0 || a.conv_lout != a.M))
+        return fail(-1, "gemm_conv: a residual needs one phase with output row = m");
     if ((int64_t)((a.M + 255) / 256) * (a.N / 256) >= (1ll << 31)) return fail(-1, "gemm_conv: grid too large");
     return launch_pp<256>(a, s);
 }

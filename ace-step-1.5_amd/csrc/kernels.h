@@ -79,8 +79,9 @@ struct GemmArgs {
     // caller provides zero rows around the input).  Column n is output channel n % conv_cout of
     // phase p = n / conv_cout (a ConvTranspose's phases side by side: W = the packed
     // [phases][conv_cout][taps·cin] taps); row m lands on output row m·conv_ostride + conv_ooff + p
-    // when that lies in [0, conv_lout): raw bf16(acc + bias) to C (if set), its Snake (sa / sib)
-    // to Cs (if set), both with row pitch ldc = conv_cout
+    // when that lies in [0, conv_lout): raw bf16(acc + bias) — or bf16(res + bf16(acc + bias)) with
+    // a residual (one phase; res may alias C) — to C (if set), its Snake (sa / sib) to Cs (if
+    // set), both with row pitch ldc = conv_cout
     const float *sa, *sib;
     bf16_t *Cs;
     int conv_cin, conv_dil, conv_a0, conv_ostride, conv_ooff, conv_cout;

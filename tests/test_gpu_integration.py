@@ -381,3 +381,25 @@ def test_install_lora_repack_vs_oracle(gpu_device, installed):
         assert rel_l2(got - base, ref - ref_base) < 0.15, rel_l2(got - base, ref - ref_base)
     h.unload_lora()
     assert torch.equal(hip(), base)
+
+
+def test_bench_two_ranks_on_one_gpu(gpu_device, tmp_path):
+    """`bench.py --gpus 2` end to end on a one-GPU box (the path the driver's multi-GPU run takes:
+    rank 0 conditions the batch of two songs and scatters it, both ranks run DiT + decode, the
+    latents are gathered, the timing is max-over-ranks): ACEHIP_DIST_BACKEND=gloo lets both ranks
+    share cuda:0 with host-staged collectives (RCCL refuses two ranks on one device).  Short songs
+    so it fits the test budget; the JSON line must report both ranks' songs."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ACEHIP_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--seconds", "10", "--no-cpu-baseline", "--no-config1"]
+    p = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stdout[-2000:]
+    d = json.loads(lines[-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"].endswith("x2"), d

@@ -159,6 +159,32 @@ def test_vae_convt_implicit_gemm(gpu_device, monkeypatch, Cin, Cout, stride, L, 
         assert rel_l2(out_s, out_s0) < 4e-3, rel_l2(out_s, out_s0)
 
 
+@pytest.mark.parametrize("C,L,raw", [(256, 1000, True), (512, 600, False), (1024, 257, True)])
+def test_vae_conv1_residual_gemm(gpu_device, monkeypatch, C, L, raw):
+    """ACEHIP_CONVP=3: the C ≥ 256 residual units' k = 1 conv with its residual (x' = x +
+    bf16(W2·y_s + b2), raw and/or snaked) as a plain GEMM on the ping-pong tile, vs torch fp32 and
+    vs convp_kernel (ACEHIP_CONVP=2)."""
+    g = torch.Generator(device=gpu_device).manual_seed(C + L)
+    x = _bf(torch.randn(L, C, device=gpu_device, generator=g))
+    w = _bf(torch.randn(C, C, 1, device=gpu_device, generator=g) / math.sqrt(C))
+    bias = _bf(torch.randn(C, device=gpu_device, generator=g) * 0.1)
+    res = _bf(torch.randn(L, C, device=gpu_device, generator=g))
+    alpha = _bf(torch.randn(C, device=gpu_device, generator=g) * 0.3)
+    beta = _bf(torch.randn(C, device=gpu_device, generator=g) * 0.3)
+    set_knob(monkeypatch, "ACEHIP_CONVP", "3")
+    out, out_s = _run_conv(0, x, w, bias, res, C, 1, 1, 1, raw, alpha, beta)
+    set_knob(monkeypatch, "ACEHIP_CONVP", "2")
+    out0, out_s0 = _run_conv(0, x, w, bias, res, C, 1, 1, 1, raw, alpha, beta)
+    torch.cuda.synchronize()
+    y = res.float() + _ref_conv(0, x, w, bias, 1, 1, 1)
+    if raw:
+        assert rel_l2(out, y) < TOL, rel_l2(out, y)
+        assert rel_l2(out, out0) < 4e-3, rel_l2(out, out0)
+    ys = snake(y, alpha, beta)
+    assert rel_l2(out_s, ys) < TOL, rel_l2(out_s, ys)
+    assert rel_l2(out_s, out_s0) < 4e-3, rel_l2(out_s, out_s0)
+
+
 def _resunit(x, x_s, L, dil, w1, bb1, a2, be2, w2, bb2, an, ben, keep):
     C = x.shape[1]
     x_out = torch.empty(L, C, device=x.device, dtype=torch.bfloat16) if keep else None
