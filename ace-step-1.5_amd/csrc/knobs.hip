@@ -38,7 +38,7 @@ Knobs read_env() {
     k.dit_graph = env_int("ACEHIP_DIT_GRAPH", 0);
     k.conv7 = env_int("ACEHIP_CONV7", 2);
     k.convt = env_int("ACEHIP_CONVT", 1);
-    k.convp = env_int("ACEHIP_CONVP", 2);
+    k.convp = env_int("ACEHIP_CONVP", 3);
     k.ru7 = env_int("ACEHIP_RU7", 2);
     k.kv_group_kib = env_int("ACEHIP_KV_GROUP_KIB", 262144);
     k.vae_snake_in = env_int("ACEHIP_VAE_SNAKE_IN", 1);
