@@ -142,7 +142,10 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
         // before its first store: the stores may alias them (in-place residual: C == res),
         // so the compiler would otherwise wait for every load right after issuing it —
         // one full memory latency per 16-B store, exposed at one wave per SIMD
-        constexpr int NP = SN / 2, CH = (CHMAX / NP) < 1 ? 1 : (CHMAX / NP);
+        // (EPI_CONV: smaller chunks — its bias and residual arrays beside the Snake parameters
+        // spilled the 256-row tile's registers at CH = 6)
+        constexpr int CHM = EPI == EPI_CONV ? 4 : CHMAX;
+        constexpr int NP = SN / 2, CH = (CHM / NP) < 1 ? 1 : (CHM / NP);
 #pragma unroll
         for (int c0 = 0; c0 < SM; c0 += CH) {
             uint4 rv[CH][NP], gv[CH][NP];
