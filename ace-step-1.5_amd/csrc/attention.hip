@@ -54,8 +54,23 @@ namespace {
 #ifndef ATT_SPLIT_HEADS
 #define ATT_SPLIT_HEADS 1  // GQA pair split into two 4-wave workgroups for short KV loops
 #endif
-#ifndef ATT_PRIO
-#define ATT_PRIO 0         // static s_setprio 1 for the younger half (waves 4-7): r02 A/B 1-3 % slower, off
+// timing experiments only (wrong results; tools/bench_attn.py against the production build):
+// attn_fwd_kernel without the QKᵀ MFMAs, the softmax VALU, the P·V MFMAs, the K/V LDS reads or the
+// per-tile barrier's wait
+#ifndef AF_X_NOQK
+#define AF_X_NOQK 0
+#endif
+#ifndef AF_X_NOSM
+#define AF_X_NOSM 0
+#endif
+#ifndef AF_X_NOPV
+#define AF_X_NOPV 0
+#endif
+#ifndef AF_X_NOREAD
+#define AF_X_NOREAD 0
+#endif
+#ifndef AF_X_NOBAR
+#define AF_X_NOBAR 0
 #endif
 #ifndef ATT_TAU
 #define ATT_TAU 8.0f       // lazy-rescale threshold (0: rescale on every new max)
@@ -88,6 +103,7 @@ struct SplitArgs {
     // its own partial with slabs c+1, c+2, … in that order and writes O.
     int sk_total = 0, sk_nt = 0, epoch = 0;
     int *flags = nullptr;   // ≥ grid ints; monotonic epochs, never reset
+    int prio = 0;           // attn_fwd_kernel<2>: static s_setprio 1 for waves 4-7 (ACEHIP_ATTN_PRIO)
 };
 
 // ds_read_b64_tr_b16 by inline asm (see pv() for why not the builtin)
@@ -109,6 +125,11 @@ __device__ __forceinline__ bf16x8 ds_read_b128(const char *lds_ptr) {
 // block are the instruction's 16-bit offset field (the tile loop is unrolled by the
 // two ring slots so both are constants) — no address VALU per read, and no hoisted
 // VGPR address per (slot, fragment), which had cost ~50 VGPRs and spills.
+__device__ __forceinline__ s16x4 opaque_s16x4() {
+    s16x4 r;
+    asm volatile("" : "=v"(r));
+    return r;
+}
 template <int OFF>
 __device__ __forceinline__ bf16x8 ds_read_b128_imm(uint32_t lane_off) {
     static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
@@ -301,7 +322,7 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     const int qi = q0 + r;
     // the younger half of the SIMD partners (waves 4-7) gets static priority
     // (MI355X_MICROARCH.md "Two waves per SIMD", item 4)
-    if (ATT_PRIO && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
+    if (sp.prio && NREP == 2 && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[qi][16s + 8hh .. +8]
     const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi, Sq - 1)) * 128;
@@ -384,6 +405,12 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     // VB: the V half of the ring slot (compile-time); key rows +32t +16s are immediates too
     auto pv_reads = [&](auto VBC, int dt, s16x4 (&rd)[2][2][2]) {
         constexpr int VB = decltype(VBC)::value;
+        if (AF_X_NOREAD) {
+            for (int a0 = 0; a0 < 2; ++a0)
+                for (int a1 = 0; a1 < 2; ++a1)
+                    for (int a2 = 0; a2 < 2; ++a2) rd[a0][a1][a2] = opaque_s16x4();
+            return;
+        }
         rd[0][0][0] = ds_read_tr16_imm<VB>(voff[dt][0]);
         rd[0][0][1] = ds_read_tr16_imm<VB>(voff[dt][1]);
         rd[0][1][0] = ds_read_tr16_imm<VB + 16 * 256>(voff[dt][0]);
@@ -407,7 +434,8 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
                 // is miscompiled by ROCm 7.2 hipcc: it keeps only the first dword)
                 const s16x8 cat = __builtin_shufflevector(rd[t][s][0], rd[t][s][1], 0, 1, 2, 3, 4, 5, 6, 7);
                 const bf16x8 vf = __builtin_bit_cast(bf16x8, cat);
-                oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
+                if (!AF_X_NOPV) oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[dt], 0, 0, 0);
+                else oacc[dt][0] += (float)vf[0] + (float)pf[t][s][1];
             }
     };
     // P·V: the reads of d-block dt+1 are in flight during the MFMAs of dt
@@ -433,7 +461,7 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     // vmcnt(0) drain
     auto tile_barrier = [&] {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if (!AF_X_NOBAR) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
     bf16x8 pf[2][2];          // P of the current tile (bf16), B operand of P·V
@@ -485,22 +513,34 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         {
             bf16x8 k0[8], k1[8];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) k0[s] = ds_read_b128_imm<KB>(koff[s]);
+            for (int s = 0; s < 8; ++s) k0[s] = AF_X_NOREAD ? qf[s] : ds_read_b128_imm<KB>(koff[s]);
             lgkm_wait8(k0);
 #pragma unroll
-            for (int s = 0; s < 8; ++s) k1[s] = ds_read_b128_imm<KB + 32 * 256>(koff[s]);
+            for (int s = 0; s < 8; ++s) k1[s] = AF_X_NOREAD ? qf[s] : ds_read_b128_imm<KB + 32 * 256>(koff[s]);
 #pragma unroll
             for (int j = 0; j < 16; ++j) { st[0][j] = 0.f; st[1][j] = 0.f; }
+            if (!AF_X_NOQK) {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[s], qf[s], st[0], 0, 0, 0);
+                for (int s = 0; s < 8; ++s) st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[s], qf[s], st[0], 0, 0, 0);
+            }
             lgkm_wait8(k1);
+            if (!AF_X_NOQK) {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[s], qf[s], st[1], 0, 0, 0);
+                for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[s], qf[s], st[1], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {       // keep the reads alive
+                    st[0][s] += (float)k0[s][0];
+                    st[1][s] += (float)k1[s][0];
+                }
+            }
         }
         // running max on raw scores (scale folded into the exp2 FMA below);
         // interior tiles of full / cross attention need no mask
         float mx = NEG;
-        if (interior) {
+        if (AF_X_NOSM) {
+            mx = m;
+        } else if (interior) {
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -536,7 +576,7 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(st[t][j], sl2, -mn));
+                const float p = AF_X_NOSM ? st[t][j] : __builtin_amdgcn_exp2f(fmaf(st[t][j], sl2, -mn));
                 st[t][j] = p;
                 rs += p;
             }
@@ -721,11 +761,6 @@ constexpr int PW_O = 0, PW_Q = 128, PW_K = 192;
 #define PW_X_NOMASK 0      // band tiles that straddle the band edge processed unmasked
 #endif
 
-__device__ __forceinline__ s16x4 opaque_s16x4() {
-    s16x4 r;
-    asm volatile("" : "=v"(r));
-    return r;
-}
 // compile-time loop: f(IC<I>{}) for I in [I0, I1)
 template <int I0, int I1, typename F>
 __device__ __forceinline__ void sfor(F &&f) {
@@ -1478,6 +1513,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         sp.flags = (int *)((char *)ws + wcus * sizeof(int) + wcus * 8 * 66 * 64 * sizeof(float));
         grid = cus;
     }
+    sp.prio = kn.attn_prio;
     if (nrep == 2) {
         attn_fwd_kernel<2><<<grid, 512, 0, s>>>(q, k, v, o, H, KV, Sq, Sk, window, sl2, o_ld, sp, kmask);
     } else if (nrep == 1) {
