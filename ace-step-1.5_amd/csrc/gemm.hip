@@ -529,13 +529,16 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
 // the barrier that opens the first read of the tile.  Two LDS tile buffers.
 // Round 4 replaced a four-phase schedule (12 / 16 MFMAs per interval, 8
 // barriers per K-tile; stamps: the 192-row loop 62 % MFMA-busy, now 80 %): DESIGN.md.
+// The body of one ping-pong tile; `bid` = the block's index in this GEMM's grid (the fused
+// main + tail launch below runs two GEMMs' grids in one) and `lds` = the kernel's 2·BUF bytes
+template <int BM>
+constexpr int pp_lds_bytes() { return 2 * (BM + 256) * 128; }
 template <int BM, int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+__device__ __forceinline__ void gemm_pp_body(const GemmArgs &a, char *lds, int bid) {
     constexpr int BN = 256, TM = BM / 2, SM = TM / 16, SMH = SM / 2;
     constexpr int ROWS = BM + BN, BUF = ROWS * 128;
     constexpr int NA = BM / 64, NB = BN / 64;                // glds per wave for A / B of one K-tile
     static_assert(SM % 2 == 0, "A half must be whole 16-row sub-tiles");
-    __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
 
     GSTAMP(0);
     GSTAMP_REAL(4);
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     const int wr = wave >> 2, wc = wave & 3;
     const int tilesM = (a.M + BM - 1) / BM, tilesN = a.N / BN;
     const int nwg = tilesM * tilesN;
-    const int wg = xcd_remap(blockIdx.x, nwg);
+    const int wg = xcd_remap(bid, nwg);
     const int per_group = GROUP_M * tilesN;
     const int gid = wg / per_group, first_m = gid * GROUP_M;
     const int gsz = min(tilesM - first_m, GROUP_M);
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     GSTAMP(2);
 
     if constexpr (EPI == EPI_HEADPOST) {
-        headpost_epilogue<BM, 8, sizeof(lds), 2>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
+        headpost_epilogue<BM, 8, 2 * BUF, 2>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
             for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -687,6 +690,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 #endif
     GSTAMP(3);
     GSTAMP_REAL(5);
+}
+
+template <int BM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[pp_lds_bytes<BM>()];
+    gemm_pp_body<BM, EPI>(a, lds, blockIdx.x);
+}
+
+// The tail-split GEMM (gemm_tail_split: whole rounds of 256-row tiles + the remaining rows as
+// one round of 128-row tiles) in ONE launch: blocks [0, nmain) run the main grid, the rest the
+// tail grid, so the tail's blocks start on CUs as the main grid's last round drains instead of
+// behind a kernel boundary (ACEHIP_GEMM_TAILFUSE)
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_split_kernel(GemmArgs a, GemmArgs t, int nmain) {
+    __shared__ __attribute__((aligned(16))) char lds[pp_lds_bytes<256>()];
+    if ((int)blockIdx.x < nmain) gemm_pp_body<256, EPI>(a, lds, blockIdx.x);
+    else gemm_pp_body<128, EPI>(t, lds, blockIdx.x - nmain);
 }
 
 // ---------------------------------------------------------------------------
@@ -1134,14 +1154,25 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     if (((a.M - M1 + 127) / 128) * (a.N / 128) > 2 * (int64_t)cus) return 1;
     GemmArgs hd = a;
     hd.M = (int)M1;
-    int rc = gemm_variant(hd, v, s);
-    if (rc) return rc;
     GemmArgs tl = a;
     tl.M = a.M - (int)M1;
     tl.A = a.A + M1 * a.lda;
     tl.C = a.C + M1 * a.ldc;
     // ACEHIP_GEMM_TAIL=1: the tail as one round of 128×256 two-phase ping-pong tiles
     const bool pp128 = knobs().gemm_tail == 1 && a.N % 256 == 0 && ((tl.M + 127) / 128) * nN <= cus;
+    if (pp128 && v == 7 && knobs().gemm_tailfuse) {
+        // both grids in one launch (the main grid's block count is a multiple of 8, so the tail
+        // blocks' XCD is their own index mod 8, as in a launch of their own)
+        const int nmain = (int)(full * cus / nN * nN), ntail = ((tl.M + 127) / 128) * (int)nN;
+        if (nmain % 8 == 0 && nmain == (hd.M / 256) * (int)nN && hd.M % 256 == 0) {
+            if (a.epi == EPI_SWIGLU) klaunch(gemm_pp_split_kernel<EPI_SWIGLU>, dim3(nmain + ntail), dim3(512), s, hd, tl, nmain);
+            else gemm_pp_split_kernel<EPI_STORE><<<nmain + ntail, 512, 0, s>>>(hd, tl, nmain);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
+    }
+    int rc = gemm_variant(hd, v, s);
+    if (rc) return rc;
     return gemm_variant(tl, pp128 ? 9 : 0, s);
 }
 

@@ -38,6 +38,7 @@ Knobs read_env() {
     k.dit_graph = env_int("ACEHIP_DIT_GRAPH", 0);
     k.conv7 = env_int("ACEHIP_CONV7", 2);
     k.convt = env_int("ACEHIP_CONVT", 1);
+    k.gemm_tailfuse = env_int("ACEHIP_GEMM_TAILFUSE", 1);
     k.attn_prio = env_int("ACEHIP_ATTN_PRIO", 0);
     k.convp = env_int("ACEHIP_CONVP", 3);
     k.ru7 = env_int("ACEHIP_RU7", 2);
