@@ -45,7 +45,8 @@ def _short(name):
 # position of the EPI template argument per GEMM kernel (gemm.hip): gemm_pp_kernel<BM, EPI, DBG,
 # SPL, SCH>, gemm_w4_kernel<BM, BN, EPI, ...>, gemm_kernel<BM, BN, WM, WN, STAGES, EPI>,
 # gemm_sk_kernel<EPI>
-EPI_POS = {"gemm_pp_kernel": 1, "gemm_w4_kernel": 2, "gemm_kernel": 5, "gemm_sk_kernel": 0}
+# gemm_pp_split_kernel<EPI>: the tail-split main + tail grids in one launch (round 5)
+EPI_POS = {"gemm_pp_kernel": 1, "gemm_w4_kernel": 2, "gemm_kernel": 5, "gemm_sk_kernel": 0, "gemm_pp_split_kernel": 0}
 
 
 def _is_swiglu(short):
