@@ -4,6 +4,9 @@ S=3000; cross Lenc=641), interleaved A/B between the working-tree library and
 any number of alternative builds (tools/ab_build.sh) in ONE process.
 
 usage: bench_attn.py [tools/ab/libacehip_ref.so ...]
+AB_ENV="VAR=VAL,..." is put into the environment after the tree library's first call, so the
+alternative builds (which read their knobs lazily at their own first call) see it and the tree
+does not: a knob A/B with a copy of the tree's own library.
 """
 import ctypes
 import json
@@ -60,6 +63,9 @@ for name, (B, H, KV, Sq, Sk, w) in SHAPES.items():
                  1 / math.sqrt(128), ff.stream_ptr()) == 0
         torch.cuda.synchronize()
         outs[ln] = o.float()
+        if ln == "tree" and os.environ.get("AB_ENV"):
+            for kv in os.environ.pop("AB_ENV").split(","):
+                os.environ[kv.split("=")[0]] = kv.split("=", 1)[1]
     for _ in range(5):                       # interleaved rounds
         for ln, f in libs:
             o = torch.empty(B, Sq, H * 128, device=dev, dtype=torch.bfloat16)
