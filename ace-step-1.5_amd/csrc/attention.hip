@@ -1374,6 +1374,312 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(const bf16_t *__restric
     }   // unit loop
 }
 
+// one wave's folded partial of attn_small_kernel: 16 values + (m, l) per lane, lane-contiguous
+// 1-KB chunks, write-through (sc1) stores / sc1 loads as slab_store / slab_load
+__device__ __forceinline__ void small_part_store(float *p, const f32x16 &a, float m, float l, int lane) {
+    float *b0 = p + lane * 4, *bm = p + 16 * 64 + lane * 2;
+    const f32x2 ml = {m, l};
+    asm volatile(
+        "global_store_dwordx4 %0, %2, off sc1\n\t"
+        "global_store_dwordx4 %0, %3, off offset:1024 sc1\n\t"
+        "global_store_dwordx4 %0, %4, off offset:2048 sc1\n\t"
+        "global_store_dwordx4 %0, %5, off offset:3072 sc1\n\t"
+        "global_store_dwordx2 %1, %6, off sc1"
+        :: "v"(b0), "v"(bm), "v"(sub4(a, 0)), "v"(sub4(a, 1)), "v"(sub4(a, 2)), "v"(sub4(a, 3)), "v"(ml)
+        : "memory");
+}
+__device__ __forceinline__ void small_part_load(const float *p, f32x16 &a, float &m, float &l, int lane) {
+    const float *b0 = p + lane * 4, *bm = p + 16 * 64 + lane * 2;
+    f32x4 v0, v1, v2, v3;
+    f32x2 ml;
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off sc1\n\t"
+        "global_load_dwordx4 %1, %5, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %5, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %5, off offset:3072 sc1\n\t"
+        "global_load_dwordx2 %4, %6, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(ml)
+        : "v"(b0), "v"(bm)
+        : "memory");
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        a[e] = v0[e];
+        a[4 + e] = v1[e];
+        a[8 + e] = v2[e];
+        a[12 + e] = v3[e];
+    }
+    m = ml[0];
+    l = ml[1];
+}
+
+// attn_small_kernel (ACEHIP_ATTN_SMALL): unmasked full / cross attention with few query rows — the
+// turbo 10 s song (Sq = 125: 8 GQA-pair units, and 2 KV tiles of self-attention or 11 of cross).
+// attn_fwd_kernel runs such a grid on 8 workgroups (self) or 8 units × 4 KV parts handed off
+// through global slabs (cross): a few CUs, or a cross-CU merge of 135 KB per part that one CU
+// reads back.  Here a workgroup is ONE head × 32 query rows and its four waves (one per SIMD)
+// take the KV tiles w, w + 4, w + 8, … each: every wave owns its K fragments (loaded straight into
+// registers in the MFMA A-operand layout, the next tile's in flight during the current one) and a
+// private two-slot LDS ring for V (LDS-DMA, read transposed), so the tile loop has no barrier;
+// the four partial (O, m, l) meet once in LDS and wave w writes head dims 32w … 32w + 31.
+// Per-tile math (Sᵀ = K·Qᵀ, exp2-domain online softmax with the lazy rescale, Oᵀ += Vᵀ·Pᵀ) is
+// attn_fwd_kernel's.
+__global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__restrict__ q, const bf16_t *__restrict__ k,
+                                                           const bf16_t *__restrict__ v, bf16_t *__restrict__ o, int H,
+                                                           int KV, int Sq, int Sk, float sl2, int64_t o_ld, int nparts,
+                                                           float *__restrict__ ws, int *__restrict__ cnt) {
+    constexpr int VT = KT * 256;                 // one V tile: 64 keys × 256 B
+    __shared__ __attribute__((aligned(16))) char lds[4 * 2 * VT];   // 128 KB: per wave two V slots
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int nq = (Sq + 31) / 32;
+    const int unit = blockIdx.x / nparts, part = blockIdx.x % nparts;
+    const int qb = unit % nq, hq = (unit / nq) % H, b = unit / (nq * H);
+    const int kvh = hq / (H / KV);
+    const int qi = qb * 32 + r;
+    bf16x8 qf[8];
+    {
+        const bf16_t *qp = q + (((int64_t)b * H + hq) * Sq + min(qi, Sq - 1)) * 128;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8 *)(qp + 16 * s + 8 * hh);
+    }
+    const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    // KV part `part` of nparts: tiles [t0, t1); wave w takes t0 + w, t0 + w + 4, …
+    const int ntall = (Sk + KT - 1) / KT, per = (ntall + nparts - 1) / nparts;
+    const int t0 = min(ntall, part * per), ntiles = min(ntall, t0 + per) - t0;
+    const int nmine = ntiles > wave ? (ntiles - wave + 3) / 4 : 0;
+    char *const vl = lds + wave * 2 * VT;
+    auto stage_v = [&](int kv0, int buf) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int row = c * 4 + (lane >> 4), pc = lane & 15;
+            const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+            glds16(vp + (int64_t)min(kv0 + row, Sk - 1) * 128 + ch * 8, vl + buf * VT + c * 1024);
+        }
+    };
+    // K fragments of keys kv0 + r (kk[0..7]) and kv0 + 32 + r (kk[8..15]): dims 16s + 8hh … +8
+    auto load_k = [&](int kv0, bf16x8 (&kk)[16]) {
+        const bf16_t *p0 = kp + (int64_t)min(kv0 + r, Sk - 1) * 128 + 8 * hh;
+        const bf16_t *p1 = kp + (int64_t)min(kv0 + 32 + r, Sk - 1) * 128 + 8 * hh;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            kk[s] = *(const bf16x8 *)(p0 + 16 * s);
+            kk[8 + s] = *(const bf16x8 *)(p1 + 16 * s);
+        }
+    };
+    const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    const uint32_t vbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)vl;
+    uint32_t voff[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int h8 = 0; h8 < 2; ++h8)
+            voff[dt][h8] = vbase + kvoff(4 * (g >> 1) + qq + 8 * h8, 4 * dt + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+
+    float m = NEG, l = 0.f;
+    f32x16 oacc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
+
+    auto tile = [&](int j, auto SLOTC, bf16x8 (&kc)[16], bf16x8 (&kn)[16]) {
+        constexpr int VB = decltype(SLOTC)::value * VT;
+        const int kv0 = (t0 + wave + 4 * j) * KT;
+        // this tile's K registers and V slot landed (issued one tile ago); the next tile's are
+        // issued now, into the other slot, whose last reads retired inside the previous tile
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (j + 1 < nmine) {
+            load_k(kv0 + 4 * KT, kn);
+            stage_v(kv0 + 4 * KT, decltype(SLOTC)::value ^ 1);
+        }
+        f32x16 st[2];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) { st[0][jj] = 0.f; st[1][jj] = 0.f; }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc[s], qf[s], st[0], 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc[8 + s], qf[s], st[1], 0, 0, 0);
+        float mx = NEG;
+        if (kv0 + KT <= Sk) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) mx = fmaxf(mx, st[t][jj]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) {
+                    const int kj = kv0 + 32 * t + (jj & 3) + 8 * (jj >> 2) + 4 * hh;
+                    const float sv = kj < Sk ? st[t][jj] : NEG;
+                    st[t][jj] = sv;
+                    mx = fmaxf(mx, sv);
+                }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+        const float mn = mx > m + ATT_TAU ? mx : m;
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const float pv = __builtin_amdgcn_exp2f(fmaf(st[t][jj], sl2, -mn));
+                st[t][jj] = pv;
+                rs += pv;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) oacc[i][jj] *= alpha;
+        }
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) pf[t][s2][jj] = (__bf16)st[t][8 * s2 + jj];
+        // Oᵀ += Vᵀ·Pᵀ: the Vᵀ reads of block dt + 1 in flight during the MFMAs of dt
+        s16x4 rd[2][2][2][2];
+        auto reads = [&](int dt, s16x4 (&x)[2][2][2]) {
+            x[0][0][0] = ds_read_tr16_imm<VB>(voff[dt][0]);
+            x[0][0][1] = ds_read_tr16_imm<VB>(voff[dt][1]);
+            x[0][1][0] = ds_read_tr16_imm<VB + 16 * 256>(voff[dt][0]);
+            x[0][1][1] = ds_read_tr16_imm<VB + 16 * 256>(voff[dt][1]);
+            x[1][0][0] = ds_read_tr16_imm<VB + 32 * 256>(voff[dt][0]);
+            x[1][0][1] = ds_read_tr16_imm<VB + 32 * 256>(voff[dt][1]);
+            x[1][1][0] = ds_read_tr16_imm<VB + 48 * 256>(voff[dt][0]);
+            x[1][1][1] = ds_read_tr16_imm<VB + 48 * 256>(voff[dt][1]);
+        };
+        auto wait = [](s16x4 (&x)[2][2][2]) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(x[0][0][0]), "+v"(x[0][0][1]), "+v"(x[0][1][0]), "+v"(x[0][1][1]),
+                           "+v"(x[1][0][0]), "+v"(x[1][0][1]), "+v"(x[1][1][0]), "+v"(x[1][1][1]));
+        };
+        auto mfmas = [&](int dt, const s16x4 (&x)[2][2][2]) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const s16x8 cat = __builtin_shufflevector(x[t][s2][0], x[t][s2][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                    oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cat), pf[t][s2],
+                                                                       oacc[dt], 0, 0, 0);
+                }
+        };
+        reads(0, rd[0]);
+        wait(rd[0]);
+        reads(1, rd[1]);
+        mfmas(0, rd[0]);
+        wait(rd[1]);
+        reads(2, rd[0]);
+        mfmas(1, rd[1]);
+        wait(rd[0]);
+        reads(3, rd[1]);
+        mfmas(2, rd[0]);
+        wait(rd[1]);
+        mfmas(3, rd[1]);
+    };
+    bf16x8 ka[16], kb[16];
+    if (nmine > 0) {
+        load_k((t0 + wave) * KT, ka);
+        stage_v((t0 + wave) * KT, 0);
+    }
+    int j = 0;
+    for (; j + 1 < nmine; j += 2) {
+        tile(j, IC<0>{}, ka, kb);
+        tile(j + 1, IC<1>{}, kb, ka);
+    }
+    if (j < nmine) tile(j, IC<0>{}, ka, kb);
+
+    // the four waves' partial (O, m, l) → LDS (the V rings are dead after the barrier), then wave w
+    // folds head dims 32w … 32w + 31 in wave order
+    __syncthreads();
+    float *const po = (float *)lds;                 // [wave][64 values][64 lanes]
+    float *const pml = (float *)(lds + 4 * 64 * 64 * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) po[(wave * 64 + i * 16 + jj) * 64 + lane] = oacc[i][jj];
+    pml[wave * 128 + lane] = m;
+    pml[wave * 128 + 64 + lane] = l;
+    __syncthreads();
+    float mw[4], lw[4], mt = NEG;
+#pragma unroll
+    for (int w2 = 0; w2 < 4; ++w2) {
+        mw[w2] = pml[w2 * 128 + lane];
+        lw[w2] = pml[w2 * 128 + 64 + lane];
+        mt = fmaxf(mt, mw[w2]);
+    }
+    float lt = 0.f;
+    f32x16 acc;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) acc[jj] = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 4; ++w2) {
+        const float a = __builtin_amdgcn_exp2f(mw[w2] - mt);   // a wave without tiles: l = 0, O = 0
+        lt = fmaf(lw[w2], a, lt);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) acc[jj] = fmaf(po[(w2 * 64 + wave * 16 + jj) * 64 + lane], a, acc[jj]);
+    }
+    if (nparts > 1) {
+        // KV parts of one unit meet in ws: each publishes its folded (O rows × dims 32w …, m, l)
+        // by write-through stores, the last arriver of the ticket folds them in part order
+        // (bit-reproducible) — 16.5 KB per part, against 135 KB per part of attn_fwd_kernel's
+        // 8-wave slabs
+        float *const wsu = ws + (int64_t)unit * nparts * (4 * 18 * 64);
+        small_part_store(wsu + ((int64_t)part * 4 + wave) * 18 * 64, acc, mt, lt, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ int s_ticket;
+        if (tid == 0) s_ticket = atomicAdd(cnt + unit, 1);
+        __syncthreads();
+        if (s_ticket != nparts - 1) return;
+        const f32x16 own = acc;
+        const float m_own = mt, l_own = lt;
+        for (int p2 = 0; p2 < nparts; ++p2) {
+            f32x16 a2 = own;
+            float m2 = m_own, l2 = l_own;
+            if (p2 != part) small_part_load(wsu + ((int64_t)p2 * 4 + wave) * 18 * 64, a2, m2, l2, lane);
+            if (p2 == 0) {
+                acc = a2;
+                mt = m2;
+                lt = l2;
+            } else {
+                const float mn = fmaxf(mt, m2);
+                const float a1 = __builtin_amdgcn_exp2f(mt - mn), b2 = __builtin_amdgcn_exp2f(m2 - mn);
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) acc[jj] = acc[jj] * a1 + a2[jj] * b2;
+                lt = lt * a1 + l2 * b2;
+                mt = mn;
+            }
+        }
+        if (tid == 0) cnt[unit] = 0;
+    }
+    if (qi < Sq) {                                  // both lanes of a row pair agree
+        const float inv = 1.0f / lt;
+        bf16_t *op = o + ((int64_t)b * Sq + qi) * o_ld + hq * 128 + 32 * wave;
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp) {
+            float vv[8];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const float a0 = acc[8 * gp + jj] * inv, a1 = acc[8 * gp + 4 + jj] * inv;
+                const float got = __shfl_xor(hh ? a0 : a1, 32, 64);
+                vv[jj] = hh ? got : a0;
+                vv[4 + jj] = hh ? a1 : got;
+            }
+            *(uint4 *)(op + 16 * gp + 8 * hh) = pack8(vv);
+        }
+    }
+}
+
 }  // namespace
 
 static int num_cus_attn() {
@@ -1439,6 +1745,27 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     const Knobs &kn = knobs();
     const int pw_mask = kn.attn_pw;
     const int kind_bit = window >= 0 ? 2 : (Sk == Sq ? 1 : 4);
+    // attn_small_kernel where its grid is at most 1.5 rounds of one-head × 32-row units (measured,
+    // tools/bench_attn.py, one process, profiles/r05an_attn_small_vs_fwd.log: B = 2 full / cross at
+    // S = 125 8.6 / 13.5 vs 15.6 / 26.7 µs, S = 375 (384 units) 21.6 / 29.1 vs 24.6 / 30.6; at
+    // S = 750 (768 units) 45.1 / 43.0 vs 34.8 / 34.0 — attn_fwd_kernel's 128-row GQA-pair units
+    // read K / V once per pair and tile, and win once the grid fills the chip)
+    const int64_t small_units = (int64_t)((Sq + 31) / 32) * H * B;
+    if (kn.attn_small && window < 0 && window != ATTN_CAUSAL && !kmask && small_units <= cus + cus / 2) {
+        const int64_t units = small_units;
+        // KV parts per unit: about one tile per wave while the grid stays within one round
+        // (ACEHIP_ATTN_SMALL=2: no parts)
+        int parts = 1;
+        const int ntall = (Sk + KT - 1) / KT;
+        if (ws && kn.attn_small == 1 && units <= std::max(1024, cus))
+            parts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(ntall + 3) / 4, cus / units, 16}));
+        attn_small_kernel<<<(unsigned)(units * parts), 256, 0, s>>>(
+            q, k, v, o, H, KV, Sq, Sk, sl2, o_ld, parts,
+            parts > 1 ? (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int)) : nullptr,
+            parts > 1 ? (int *)ws : nullptr);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (grp == 2 && !kmask && window != ATTN_CAUSAL && (pw_mask & kind_bit)) {
         const int units = nq * KV * B;
         SplitArgs sp{nq, units, 1, nullptr, nullptr};

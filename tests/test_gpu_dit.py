@@ -112,6 +112,41 @@ def test_attention_tail_split(gpu_device, monkeypatch, cus, window, pw):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
+@pytest.mark.parametrize("B,H,KV,Sq,Sk,cus", [(1, 16, 8, 125, 641, 0), (1, 16, 8, 125, 125, 0),
+                                               (2, 16, 8, 125, 641, 0), (1, 16, 8, 1, 641, 0),
+                                               (1, 2, 1, 33, 65, 0), (3, 4, 2, 77, 1000, 0),
+                                               (1, 16, 16, 200, 2000, 0), (1, 16, 8, 125, 641, 100),
+                                               (1, 4, 2, 31, 3000, 64), (1, 2, 1, 40, 1, 0)])
+def test_attention_small(gpu_device, monkeypatch, B, H, KV, Sq, Sk, cus):
+    """attn_small_kernel (few-unit unmasked full / cross attention, the turbo 10 s song): one head
+    × 32 query rows per workgroup, KV tiles interleaved over four waves, their partials folded in
+    LDS, and the unit's KV parts (ACEHIP_ATTN_SMALL=1: about one tile per wave, 1 to 16 parts)
+    folded through the workspace in part order.  Against the fp32 reference; bit-reproducible
+    over launches (the tickets self-reset); parts vs no parts (=2) within rounding."""
+    if cus:
+        set_knob(monkeypatch, "ACEHIP_ATTN_CUS", str(cus))
+    ff = _lib()
+    g = torch.Generator(device="cpu").manual_seed(Sq * 7 + Sk + B)
+    q = torch.randn(B, H, Sq, 128, generator=g).to(gpu_device, torch.bfloat16)
+    k = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
+    v = torch.randn(B, KV, Sk, 128, generator=g).to(gpu_device, torch.bfloat16)
+    ref = _attn_ref(q, k, v, -1).transpose(1, 2).reshape(B, Sq, H * 128).float().cpu()
+    outs = {}
+    for mode in ("1", "2"):
+        set_knob(monkeypatch, "ACEHIP_ATTN_SMALL", mode)
+        runs = []
+        for _ in range(3):
+            o = torch.full((B, Sq, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+            ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, Sq, Sk,
+                                                    -1, 1 / math.sqrt(128), ff.stream_ptr()))
+            torch.cuda.synchronize()
+            runs.append(o)
+        assert torch.equal(runs[0], runs[1]) and torch.equal(runs[0], runs[2])
+        assert rel_l2(runs[0].float().cpu(), ref) < 1e-2
+        outs[mode] = runs[0].float().cpu()
+    assert rel_l2(outs["1"], outs["2"]) < 1e-2
+
+
 @pytest.mark.parametrize("cus,B,H,KV,S,window", [(16, 2, 4, 2, 1000, 128), (37, 2, 4, 2, 1000, 128),
                                                   (100, 1, 16, 8, 777, 64), (7, 1, 2, 1, 450, 200),
                                                   (0, 2, 16, 8, 3000, 128), (0, 4, 16, 8, 3000, 128)])

@@ -19,6 +19,7 @@ TAG=${1:?tag}; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 n_pmc=0
+n_py=1
 run() {  # name seconds cmd...
     local name=$1 secs=$2; shift 2
     local log=gpurun_out/${TAG}_${name}.log
@@ -61,7 +62,9 @@ for step in "$@"; do
         py)
             script=${arg%%=*}; pargs=""
             [ "$script" != "$arg" ] && pargs=${arg#*=}
-            run "$(basename "$script" .py)" 900 python -u "$script" $pargs ;;
+            name=$(basename "$script" .py)
+            [ -e "gpurun_out/${TAG}_${name}.log" ] && name="${name}_$((++n_py))"
+            run "$name" 900 python -u "$script" $pargs ;;
         pystats)
             script=${arg%%=*}; pargs=""
             [ "$script" != "$arg" ] && pargs=${arg#*=}
