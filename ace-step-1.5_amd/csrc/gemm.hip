@@ -137,15 +137,84 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
             }
         }
     }
-    if constexpr (EPI != EPI_SWIGLU) {
+    if constexpr (EPI == EPI_CONV) {
+        // vmcnt counts loads and stores together, so a load issued after a store is waited with
+        // that store: every per-column operand (bias, Snake a / 1/b) is loaded once, before the
+        // first store, and each row group's residual before the previous row group's stores.
+        // The chunked form of the other epilogues (below) loaded the Snake parameters after each
+        // store — one store latency in front of every 16-B parameter load: k = 1 C = 256 tile
+        // epilogue 64.6 k → 41.0 k cycles, k = 7 C = 256 → 10.7 k (profiles/r05aq_conv_stamps_
+        // before.log, r05ar_conv_stamps_after.log); 240 s decode 34.87 → 32.84 ms, bit-identical
+        // (r05ar_ab_vae.log).  What is left of the k = 1 epilogue is its 256 KB of stores per
+        // tile (raw x' and its Snake): staging the residual tile in LDS first measured ±0
+        // (r05as_ab_env_vae_reslds.log)
+        constexpr int NP = SN / 2;
+        uint4 bz[NP];
+        float sav[NP][8], sbv[NP][8];
+        int colv[NP], phv[NP];
+#pragma unroll
+        for (int jp = 0; jp < NP; ++jp) {
+            const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
+            phv[jp] = n / a.conv_cout;
+            colv[jp] = n - phv[jp] * a.conv_cout;
+            bz[jp] = a.bias ? *(const uint4 *)(a.bias + colv[jp]) : make_uint4(0, 0, 0, 0);
+            if (a.Cs) {
+                const float4 a0 = *(const float4 *)(a.sa + colv[jp]), a1 = *(const float4 *)(a.sa + colv[jp] + 4);
+                const float4 b0 = *(const float4 *)(a.sib + colv[jp]), b1 = *(const float4 *)(a.sib + colv[jp] + 4);
+                sav[jp][0] = a0.x; sav[jp][1] = a0.y; sav[jp][2] = a0.z; sav[jp][3] = a0.w;
+                sav[jp][4] = a1.x; sav[jp][5] = a1.y; sav[jp][6] = a1.z; sav[jp][7] = a1.w;
+                sbv[jp][0] = b0.x; sbv[jp][1] = b0.y; sbv[jp][2] = b0.z; sbv[jp][3] = b0.w;
+                sbv[jp][4] = b1.x; sbv[jp][5] = b1.y; sbv[jp][6] = b1.z; sbv[jp][7] = b1.w;
+            }
+        }
+        // residual (k = 1 convs of the C ≥ 256 residual units; one phase, so the output row is
+        // m; res may be C): row group i + 1's loads issued before row group i's stores
+        uint4 gv[2][NP];
+        auto load_res = [&](int i, uint4 (&g)[NP]) {
+            const int m = min(row0 + i * 16 + fr, a.M - 1);
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp)
+                g[jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos);
+        };
+        if (a.res) load_res(0, gv[0]);
+#pragma unroll
+        for (int i = 0; i < SM; ++i) {
+            if (a.res && i + 1 < SM) load_res(i + 1, gv[(i + 1) & 1]);
+            const int m = row0 + i * 16 + fr;
+            const bool live = m < a.M;           // rows past M still join the lane exchange
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp) {
+                float o[8];
+                pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
+                if (a.bias) {
+                    float bb[8];
+                    unpack8(bz[jp], bb);
+                    add_n<8>(o, bb);
+                }
+                // the conv output rounded to bf16 (raw), then its Snake (conv.hip)
+                rbf_n<8>(o);
+                if (a.res) {                     // x' = bf16(x + bf16(acc + b))
+                    float rr[8];
+                    unpack8(gv[i & 1][jp], rr);
+                    add_n<8>(o, rr);
+                    rbf_n<8>(o);
+                }
+                const int64_t orow = (int64_t)m * a.conv_ostride + a.conv_ooff + phv[jp];
+                const bool ok = live && orow >= 0 && orow < a.conv_lout;
+                if (a.C && ok) *(uint4 *)(a.C + orow * a.ldc + colv[jp]) = pack8(o);
+                if (a.Cs) {
+                    float sn[8];
+                    snake_n<8>(o, sav[jp], sbv[jp], sn);
+                    if (ok) *(uint4 *)(a.Cs + orow * a.ldc + colv[jp]) = pack8(sn);
+                }
+            }
+        }
+    } else if constexpr (EPI != EPI_SWIGLU) {
         // operand loads (residual, gate, bias) of a chunk of CH row groups are all issued
         // before its first store: the stores may alias them (in-place residual: C == res),
         // so the compiler would otherwise wait for every load right after issuing it —
         // one full memory latency per 16-B store, exposed at one wave per SIMD
-        // (EPI_CONV: smaller chunks — its bias and residual arrays beside the Snake parameters
-        // spilled the 256-row tile's registers at CH = 6)
-        constexpr int CHM = EPI == EPI_CONV ? 4 : CHMAX;
-        constexpr int NP = SN / 2, CH = (CHM / NP) < 1 ? 1 : (CHM / NP);
+        constexpr int NP = SN / 2, CH = (CHMAX / NP) < 1 ? 1 : (CHMAX / NP);
 #pragma unroll
         for (int c0 = 0; c0 < SM; c0 += CH) {
             uint4 rv[CH][NP], gv[CH][NP];
@@ -159,11 +228,6 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
                     if constexpr (EPI == EPI_STORE) {
                         if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n);
-                    } else if constexpr (EPI == EPI_CONV) {
-                        if (a.bias) rv[ii][jp] = *(const uint4 *)(a.bias + n % a.conv_cout);
-                        // residual (k = 1 convs of the C ≥ 256 residual units; one phase, so the
-                        // output row is m): loaded with the chunk, before any store — res may be C
-                        if (a.res) gv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
                     } else {
                         rv[ii][jp] = *(const uint4 *)(a.res + (int64_t)m * a.ldr + n);
                         if constexpr (EPI == EPI_GATED_RES)
@@ -182,37 +246,12 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs &a, const f32x4 (&a
                     float o[8];
                     pair8(acc[i][2 * jp], acc[i][2 * jp + 1], odd, o);
                     const int n = col0 + (2 * jp + (odd ? 1 : 0)) * 16 + cpos;
-                    if constexpr (EPI == EPI_STORE || EPI == EPI_CONV) {
+                    if constexpr (EPI == EPI_STORE) {
                         if (a.bias) {
                             float bb[8];
                             unpack8(rv[ii][jp], bb);
 #pragma unroll
                             for (int r = 0; r < 8; ++r) o[r] += bb[r];
-                        }
-                        if constexpr (EPI == EPI_CONV) {
-                            // the conv output rounded to bf16 (raw), then its Snake (conv.hip)
-                            rbf_n<8>(o);
-                            if (a.res) {                     // x' = bf16(x + bf16(acc + b))
-                                float rr[8];
-                                unpack8(gv[ii][jp], rr);
-#pragma unroll
-                                for (int r = 0; r < 8; ++r) o[r] = rr[r] + o[r];
-                                rbf_n<8>(o);
-                            }
-                            const int ph = n / a.conv_cout, col = n - ph * a.conv_cout;
-                            const int64_t orow = (int64_t)m * a.conv_ostride + a.conv_ooff + ph;
-                            const bool ok = live && orow >= 0 && orow < a.conv_lout;
-                            if (a.C && ok) *(uint4 *)(a.C + orow * a.ldc + col) = pack8(o);
-                            if (a.Cs) {
-                                const float4 a0 = *(const float4 *)(a.sa + col), a1 = *(const float4 *)(a.sa + col + 4);
-                                const float4 b0 = *(const float4 *)(a.sib + col), b1 = *(const float4 *)(a.sib + col + 4);
-                                const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                                const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-                                float sn[8];
-                                snake_n<8>(o, av, bv, sn);
-                                if (ok) *(uint4 *)(a.Cs + orow * a.ldc + col) = pack8(sn);
-                            }
-                            continue;
                         }
                     } else {
                         float rr[8];

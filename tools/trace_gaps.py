@@ -61,6 +61,13 @@ def main():
         key = (a, b)
         n, tot = agg.get(key, (0, 0))
         agg[key] = (n + 1, tot + g)
+    tot = {}
+    for kid, s_, e_ in win:
+        n, t = tot.get(names.get(kid, "?"), (0, 0))
+        tot[names.get(kid, "?")] = (n + 1, t + (e_ - s_))
+    print("kernel time inside the window (top 25):")
+    for nm, (n, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"  {t / 1e6:8.3f} ms  {n:6d} x {t / n / 1e3:8.1f} us  {nm}")
     print("largest idle totals by (before → after):")
     for (a, b), (n, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:15]:
         print(f"  {tot / 1e3:9.1f} us over {n:5d} gaps  {a}  →  {b}")
