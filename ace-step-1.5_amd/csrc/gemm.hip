@@ -978,11 +978,11 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
         case EPI_RES: gemm_pp_kernel<BM, EPI_RES><<<tiles, 512, 0, s>>>(a); break;
         case EPI_SWIGLU: klaunch(gemm_pp_kernel<BM, EPI_SWIGLU>, dim3(tiles), dim3(512), s, a); break;
         case EPI_CONV:
-            if constexpr (BM == 256) {
+            if constexpr (BM == 256 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_CONV><<<tiles, 512, 0, s>>>(a);
                 break;
             }
-            return fail(-1, "gemm: the conv epilogue runs on the 256-row ping-pong tile");
+            return fail(-1, "gemm: the conv epilogue runs on the 256- or 128-row ping-pong tile");
         case EPI_HEADPOST:
             if constexpr (BM == 192 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
@@ -1215,6 +1215,14 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     return gemm_variant(tl, pp128 ? 9 : 0, s);
 }
 
+// the conv epilogue on 64-row ping-pong tiles
+static int launch_conv64(const GemmArgs &a, hipStream_t s) {
+    const int tiles = ((a.M + 63) / 64) * (a.N / 256);
+    gemm_pp_kernel<64, EPI_CONV><<<tiles, 512, 0, s>>>(a);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int gemm_conv(const GemmArgs &a, hipStream_t s) {
     if (a.epi != EPI_CONV || (!a.C && !a.Cs) || (a.Cs && (!a.sa || !a.sib)) || a.conv_cin <= 0 || a.conv_dil < 1 ||
         a.conv_ostride < 1 || a.conv_cout <= 0 || a.conv_cout % 8 || a.N % a.conv_cout || a.conv_lout <= 0 || a.M <= 0)
@@ -1224,6 +1232,13 @@ int gemm_conv(const GemmArgs &a, hipStream_t s) {
     if (a.res && (a.N != a.conv_cout || a.ldr != a.N || a.conv_ostride != 1 || a.conv_ooff != 0 || a.conv_lout != a.M))
         return fail(-1, "gemm_conv: a residual needs one phase with output row = m");
     if ((int64_t)((a.M + 255) / 256) * (a.N / 256) >= (1ll << 31)) return fail(-1, "gemm_conv: grid too large");
+    // short activations (a 10 s decode's C = 1024 / 512 blocks: 40 / 118 tiles of 256 rows on
+    // 256 CUs): 128-row tiles double the grid, 64-row tiles (80 KB of LDS, 118 VGPRs: two blocks
+    // per CU) quadruple it.  10 s decode 2.13 → 1.96 (128) → 1.91 ms (64 below a quarter of the
+    // chip), bit-identical (profiles/r05az_ab_vae_small_tiles.log; ACEHIP_CONV_BM128)
+    const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
+    if (knobs().conv_bm128 == 2 && t256 * 4 <= num_cus()) return launch_conv64(a, s);
+    if (knobs().conv_bm128 && t256 * 2 <= num_cus()) return launch_pp<128>(a, s);
     return launch_pp<256>(a, s);
 }
 

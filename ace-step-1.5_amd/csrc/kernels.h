@@ -30,6 +30,7 @@ struct Knobs {
     int gemm_tailfuse = 1;    // ACEHIP_GEMM_TAILFUSE: the tail-split GEMM's main and tail grids in one launch
     int convt = 1;            // ACEHIP_CONVT: 1 ConvTranspose (N % 256 == 0, padded input) as an implicit GEMM, 0 conv_gemm_kernel
     int conv7 = 2;            // ACEHIP_CONV7: k = 7 VAE convs — 2 implicit GEMM on the ping-pong tile (C ≥ 256, padded input), 1 halo-staged conv7_kernel
+    int conv_bm128 = 2;       // ACEHIP_CONV_BM128: GEMM convs whose 256-row grid fills ≤ 1/2 of the chip on 128-row tiles, ≤ 1/4 on 64-row (2; 1: 128 only; 0: 256 always)
     int convp = 3;            // ACEHIP_CONVP: 0 none, 1 all, 2 k = 1 convs on convp_kernel, 3 k = 1 convs with N % 256 == 0 on the ping-pong GEMM (the rest on conv_gemm_kernel)
     int ru7 = 2;              // ACEHIP_RU7: C = 128 residual unit — 2 ru8_kernel (256-row tiles), 1 ru7_kernel, 0 conv7
     int vae_snake_in = 1;     // ACEHIP_VAE_SNAKE_IN: C = 128 decoder blocks without x_s tensors (ru8 SIN)

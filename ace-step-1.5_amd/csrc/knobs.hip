@@ -42,6 +42,7 @@ Knobs read_env() {
     k.gemm_tailfuse = env_int("ACEHIP_GEMM_TAILFUSE", 1);
     k.attn_prio = env_int("ACEHIP_ATTN_PRIO", 0);
     k.convp = env_int("ACEHIP_CONVP", 3);
+    k.conv_bm128 = env_int("ACEHIP_CONV_BM128", 2);
     k.ru7 = env_int("ACEHIP_RU7", 2);
     k.kv_group_kib = env_int("ACEHIP_KV_GROUP_KIB", 262144);
     k.vae_snake_in = env_int("ACEHIP_VAE_SNAKE_IN", 1);
