@@ -1427,7 +1427,8 @@ __device__ __forceinline__ void small_part_load(const float *p, f32x16 &a, float
 __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__restrict__ q, const bf16_t *__restrict__ k,
                                                            const bf16_t *__restrict__ v, bf16_t *__restrict__ o, int H,
                                                            int KV, int Sq, int Sk, float sl2, int64_t o_ld, int nparts,
-                                                           float *__restrict__ ws, int *__restrict__ cnt) {
+                                                           float *__restrict__ ws, int *__restrict__ cnt,
+                                                           const uint8_t *__restrict__ kmask) {
     constexpr int VT = KT * 256;                 // one V tile: 64 keys × 256 B
     __shared__ __attribute__((aligned(16))) char lds[4 * 2 * VT];   // 128 KB: per wave two V slots
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1445,6 +1446,9 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
     }
     const bf16_t *kp = k + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
     const bf16_t *vp = v + ((int64_t)b * KV + kvh) * (int64_t)Sk * 128;
+    // key-padding mode (the condition encoders): excluded keys score NEG, keys past Sk PAST, as
+    // attn_fwd_kernel's masked mode — an all-excluded row softmaxes uniformly over its Sk keys
+    const uint8_t *km = kmask ? kmask + (int64_t)b * Sk : nullptr;
     // KV part `part` of nparts: tiles [t0, t1); wave w takes t0 + w, t0 + w + 4, …
     const int ntall = (Sk + KT - 1) / KT, per = (ntall + nparts - 1) / nparts;
     const int t0 = min(ntall, part * per), ntiles = min(ntall, t0 + per) - t0;
@@ -1502,7 +1506,7 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
 #pragma unroll
         for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc[8 + s], qf[s], st[1], 0, 0, 0);
         float mx = NEG;
-        if (kv0 + KT <= Sk) {
+        if (!km && kv0 + KT <= Sk) {
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1513,7 +1517,9 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
 #pragma unroll
                 for (int jj = 0; jj < 16; ++jj) {
                     const int kj = kv0 + 32 * t + (jj & 3) + 8 * (jj >> 2) + 4 * hh;
-                    const float sv = kj < Sk ? st[t][jj] : NEG;
+                    const bool inr = kj < Sk;
+                    float sv = inr ? st[t][jj] : NEG;
+                    if (km) sv = inr ? (km[kj] != 0 ? sv : NEG) : PAST;   // km is kernel-uniform
                     st[t][jj] = sv;
                     mx = fmaxf(mx, sv);
                 }
@@ -1751,7 +1757,8 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // S = 750 (768 units) 45.1 / 43.0 vs 34.8 / 34.0 — attn_fwd_kernel's 128-row GQA-pair units
     // read K / V once per pair and tile, and win once the grid fills the chip)
     const int64_t small_units = (int64_t)((Sq + 31) / 32) * H * B;
-    if (kn.attn_small && window < 0 && window != ATTN_CAUSAL && !kmask && small_units <= cus + cus / 2) {
+    if (kn.attn_small && window < 0 && window != ATTN_CAUSAL && small_units <= cus + cus / 2 &&
+        (!kmask || kn.attn_small_mask)) {
         const int64_t units = small_units;
         // KV parts per unit: about one tile per wave while the grid stays within one round
         // (ACEHIP_ATTN_SMALL=2: no parts)
@@ -1762,7 +1769,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         attn_small_kernel<<<(unsigned)(units * parts), 256, 0, s>>>(
             q, k, v, o, H, KV, Sq, Sk, sl2, o_ld, parts,
             parts > 1 ? (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int)) : nullptr,
-            parts > 1 ? (int *)ws : nullptr);
+            parts > 1 ? (int *)ws : nullptr, kmask);
         HIP_TRY(hipGetLastError());
         return 0;
     }

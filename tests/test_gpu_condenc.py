@@ -8,7 +8,7 @@ rel-L2 <= 2.5 %, cosine >= 0.999; masks and packing order exact."""
 import pytest
 import torch
 
-from conftest import cosine, golden_manifest, load_golden, rel_l2
+from conftest import cosine, golden_manifest, load_golden, rel_l2, set_knob
 
 from acehip.config import DiTConfig
 from acehip.weights import synth_condenc_weights
@@ -46,6 +46,42 @@ def test_masked_attention(gpu_device, H, KV, S, window, valid):
     assert rel_l2(o, ref) < 1e-2
     # rows with no admissible key: uniform over every key (finite finfo.min semantics)
     assert torch.isfinite(o).all()
+
+
+@pytest.mark.parametrize("H,KV,S,valid", [(16, 8, 300, [0, 217]), (2, 1, 1000, [999, 3]), (4, 2, 77, [77, 1]),
+                                           (16, 16, 250, [250, 0])])
+def test_masked_attention_small(gpu_device, monkeypatch, H, KV, S, valid):
+    """Key-padding-masked full attention on attn_small_kernel (ACEHIP_ATTN_SMALL_MASK, the
+    encoders' short grids; KV parts through the workspace at S = 1000): against SDPA
+    with the reference's additive mask — an all-masked row (valid 0) is uniform over its S keys —
+    and against attn_fwd_kernel's masked mode (=0)."""
+    from acehip import _ffi as ff
+    B = len(valid)
+    g = torch.Generator().manual_seed(S * 3 + H)
+    q = torch.randn(B, H, S, 128, generator=g).bfloat16()
+    k = torch.randn(B, KV, S, 128, generator=g).bfloat16()
+    v = torch.randn(B, KV, S, 128, generator=g).bfloat16()
+    m = torch.zeros(B, S, dtype=torch.long)
+    for b, n in enumerate(valid):
+        m[b, :n] = 1
+    mask = co.create_4d_mask(S, torch.float32, m, None)
+    rep = H // KV
+    ref = torch.nn.functional.scaled_dot_product_attention(
+        q.float(), k.float().repeat_interleave(rep, 1), v.float().repeat_interleave(rep, 1), attn_mask=mask,
+        scale=128 ** -0.5).transpose(1, 2).reshape(B, S, H * 128)
+    qd, kd, vd = (t.to(gpu_device).contiguous() for t in (q, k, v))
+    km = m.to(gpu_device, torch.uint8).contiguous()
+    outs = {}
+    for mode in ("1", "0"):
+        set_knob(monkeypatch, "ACEHIP_ATTN_SMALL_MASK", mode)
+        o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_attention_masked_bf16(ff.ptr(qd), ff.ptr(kd), ff.ptr(vd), ff.ptr(o), B, H, KV, S,
+                                                       S, -1, 128 ** -0.5, ff.ptr(km), ff.stream_ptr()))
+        torch.cuda.synchronize()
+        outs[mode] = o.float().cpu()
+        assert torch.isfinite(outs[mode]).all()
+        assert rel_l2(outs[mode], ref) < 1e-2
+    assert rel_l2(outs["1"], outs["0"]) < 1e-2
 
 
 def _setup(name, gpu_device):
