@@ -1086,6 +1086,10 @@ int gemm_pick_variant(int64_t M, int N) {
     const int cus = num_cus();
     const int64_t t7 = ((M + 255) / 256) * (N / 256), t8 = ((M + 191) / 192) * (N / 256);
     if (t8 <= cus / 2) return 0;
+    // one partial round of 192-row tiles (M ≈ 500: the 20 s song's CFG batch, the lyric
+    // encoder's SwiGLU): 128-row tiles still fit one round and finish sooner (ACEHIP_GEMM_PP128)
+    const int64_t t9 = ((M + 127) / 128) * (N / 256);
+    if (knobs().gemm_pp128 && t8 <= cus && t9 <= cus) return 9;
     const double c7 = (double)((t7 + cus - 1) / cus) * 1.093, c8 = (double)((t8 + cus - 1) / cus);
     return c7 < c8 ? 7 : 8;
 }

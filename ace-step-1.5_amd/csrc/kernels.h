@@ -28,6 +28,7 @@ struct Knobs {
     int dit_dedup = 1;        // ACEHIP_DIT_DEDUP: layer-0 CFG row dedup
     int dit_graph = 0;        // ACEHIP_DIT_GRAPH: HIP-graph replay of the forward body
     int attn_prio = 0;        // ACEHIP_ATTN_PRIO: attn_fwd_kernel<2> waves 4-7 at s_setprio 1 (the guide's static priority)
+    int gemm_pp128 = 1;       // ACEHIP_GEMM_PP128: a one-round 192-row grid whose 128-row grid also fits one round runs on 128-row tiles
     int gemm_tailfuse = 1;    // ACEHIP_GEMM_TAILFUSE: the tail-split GEMM's main and tail grids in one launch
     int convt = 1;            // ACEHIP_CONVT: 1 ConvTranspose (N % 256 == 0, padded input) as an implicit GEMM, 0 conv_gemm_kernel
     int conv7 = 2;            // ACEHIP_CONV7: k = 7 VAE convs — 2 implicit GEMM on the ping-pong tile (C ≥ 256, padded input), 1 halo-staged conv7_kernel
