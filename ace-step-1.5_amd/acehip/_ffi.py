@@ -20,7 +20,7 @@ ABI_VERSION = 400
 
 # every symbol include/acehip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "acehip_get_version", "acehip_last_error", "acehip_reload_knobs",
+    "acehip_get_version", "acehip_last_error", "acehip_reload_knobs", "acehip_build_hash",
     "acehip_dit_create", "acehip_dit_set_weight", "acehip_dit_finalize",
     "acehip_dit_set_condition", "acehip_dit_set_uniform_rows", "acehip_dit_forward", "acehip_dit_destroy",
     "acehip_dit_set_graph", "acehip_dit_set_timesteps", "acehip_dit_forward_step",
@@ -67,6 +67,7 @@ def _declare(lib):
     sig = {
         "acehip_get_version": (c_int, []),
         "acehip_last_error": (c_char_p, []),
+        "acehip_build_hash": (c_char_p, []),
         "acehip_reload_knobs": (c_int, []),
         "acehip_dit_create": (c_int, [c_int, POINTER(DiTCfg), POINTER(c_void_p)]),
         "acehip_dit_set_weight": (c_int, [P, c_char_p, P, c_int, c_int, POINTER(c_int64), c_int]),
@@ -136,8 +137,34 @@ def lib():
         if v != ABI_VERSION:
             raise RuntimeError(f"acehip: {LIB_PATH} has ABI version {v}, this binding expects "
                                f"{ABI_VERSION} (include/acehip.h); rebuild the library")
+        built, tree = build_hash(handle), source_hash()
+        if tree is not None and built != tree:
+            raise RuntimeError(f"acehip: {LIB_PATH} was built from native sources {built}, the tree beside "
+                               f"it is {tree}; rebuild the library (make -C ace-step-1.5_amd)")
         _LIB = handle
     return _LIB
+
+
+def build_hash(handle=None) -> str:
+    """The native-source hash compiled into the library (acehip_build_hash)."""
+    h = handle if handle is not None else lib()
+    if not hasattr(h, "acehip_build_hash"):
+        return "none"
+    h.acehip_build_hash.restype = c_char_p
+    return h.acehip_build_hash().decode()
+
+
+def source_hash():
+    """The native-source hash of the tree this package sits in (None if the sources are absent,
+    e.g. an installed wheel: then only the ABI version is checked)."""
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "native_hash.py")
+    if not os.path.exists(script):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_acehip_native_hash", script)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.native_hash()
 
 
 def missing_exports():

@@ -23,6 +23,7 @@ own ``prepare_condition`` when one is given, or raise).
 """
 from __future__ import annotations
 
+import logging
 import math
 from typing import Callable, Dict, Optional, Tuple
 
@@ -31,6 +32,8 @@ import torch
 from . import _ffi
 from ._ffi import ACEHIP_BF16, ACEHIP_F32, check, lib, ptr, shape_arg, stream_ptr
 from .config import DiTConfig
+
+log = logging.getLogger("acehip")
 
 
 class EncoderStack:
@@ -459,11 +462,54 @@ class HipPrepareCondition:
     Covers that need the tokenizer go to ``fallback`` (the reference's own
     ``prepare_condition``) or raise."""
 
+    # the inputs the result depends on (``attention_mask`` only feeds tokenize's pooled mask,
+    # which prepare_condition discards: base:1586-1590,1645)
+    _MEMO_KEYS = ("text_hidden_states", "text_attention_mask", "lyric_hidden_states", "lyric_attention_mask",
+                  "refer_audio_acoustic_hidden_states_packed", "refer_audio_order_mask", "hidden_states",
+                  "silence_latent", "src_latents", "chunk_masks", "is_covers", "precomputed_lm_hints_25Hz",
+                  "audio_codes")
+
     def __init__(self, encoder: ConditionEncoder, fallback: Optional[Callable] = None,
                  tokenizer: Optional[AudioTokenizer] = None, detokenizer: Optional[AudioDetokenizer] = None):
         self.encoder = encoder
         self.fallback = fallback
         self.tokenizer, self.detokenizer = tokenizer, detokenizer
+        self._memo = None
+        self.passes = 0          # encoder passes run (tests count one per request through install())
+
+    # -- one encoder pass per request ------------------------------------------------------------
+    # The handler conditions the request itself (service_generate_execute.py:123-142) and the
+    # reference generate_audio conditions it AGAIN from the same payload tensors (base:1820).
+    # install() binds ``record`` to the handler's call and ``consume`` to generate_audio's: the
+    # second call reuses the first's outputs when every input is the same tensor object (same
+    # storage, shape and — where torch tracks one — version); the memo is single-use, so a later
+    # request (or a direct generate_audio call, as bench.py makes) always runs the encoders.
+    @classmethod
+    def _key(cls, kw):
+        parts = []
+        for name in cls._MEMO_KEYS:
+            v = kw.get(name)
+            if isinstance(v, torch.Tensor):
+                try:
+                    ver = v._version
+                except RuntimeError:             # inference tensors carry no version counter
+                    ver = None
+                parts.append((name, id(v), v.data_ptr(), tuple(v.shape), v.dtype, ver))
+            else:
+                parts.append((name, None if v is None else ("obj", id(v))))
+        return tuple(parts)
+
+    def record(self, **kw):
+        out = self(**kw)
+        # strong references keep the keyed objects (and so their ids) alive while the memo lives
+        self._memo = (self._key(kw), [kw.get(n) for n in self._MEMO_KEYS], out)
+        return out
+
+    def consume(self, **kw):
+        memo, self._memo = self._memo, None
+        if memo is not None and memo[0] == self._key(kw):
+            return memo[2]
+        return self(**kw)
 
     def tokenize(self, x, silence_latent):
         """AceStepConditionGenerationModel.tokenize (base:1580-1591): pad T to a
@@ -493,6 +539,8 @@ class HipPrepareCondition:
             if self.fallback is None:
                 raise NotImplementedError("acehip: cover conditioning needs the FSQ audio tokenizer "
                                           "(pass precomputed_lm_hints_25Hz or a reference fallback)")
+            log.warning("acehip: cover conditioning without an audio tokenizer handle — delegating this "
+                        "request to the reference prepare_condition (PyTorch, not libacehip)")
             return self.fallback(
                 text_hidden_states=text_hidden_states, text_attention_mask=text_attention_mask,
                 lyric_hidden_states=lyric_hidden_states, lyric_attention_mask=lyric_attention_mask,
@@ -502,6 +550,7 @@ class HipPrepareCondition:
                 chunk_masks=chunk_masks, is_covers=is_covers,
                 precomputed_lm_hints_25Hz=precomputed_lm_hints_25Hz, audio_codes=audio_codes)
         dtype = hidden_states.dtype
+        self.passes += 1
         enc, enc_mask = self.encoder(text_hidden_states, text_attention_mask, lyric_hidden_states,
                                      lyric_attention_mask, refer_audio_acoustic_hidden_states_packed,
                                      refer_audio_order_mask)

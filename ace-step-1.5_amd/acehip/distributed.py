@@ -246,6 +246,30 @@ class SongParallel:
 # service_generate_execute.py:62-105, is conditioning, which rank 0 turns into tensors)
 _SAMPLER_KW = ("infer_steps", "diffusion_guidance_sale", "shift", "infer_method", "use_adg", "cfg_interval_start",
                "cfg_interval_end", "audio_cover_strength", "cover_noise_strength", "timesteps")
+# generate_audio keywords rank 0 consumes into the scattered tensors (conditioning, noise seed)
+_CONDITION_KW = ("text_hidden_states", "text_attention_mask", "lyric_hidden_states", "lyric_attention_mask",
+                 "refer_audio_acoustic_hidden_states_packed", "refer_audio_order_mask", "src_latents", "chunk_masks",
+                 "is_covers", "silence_latent", "attention_mask", "seed", "non_cover_text_hidden_states",
+                 "non_cover_text_attention_mask", "precomputed_lm_hints_25Hz", "audio_codes",
+                 "encoder_hidden_states", "encoder_attention_mask", "context_latents")
+
+
+def _rank_kwargs(kw: dict) -> dict:
+    """The keywords every rank's generate_audio gets: the sampler keywords plus any other
+    non-tensor keyword the caller passed (e.g. turbo's ``fix_nfe``, ``use_progress_bar``), so a
+    call behaves the same through the pipeline as on ``AceStepDiTBackend.generate_audio``
+    directly.  An unknown TENSOR keyword cannot be split per song and is refused."""
+    meta = {}
+    for k, v in kw.items():
+        if k in _CONDITION_KW:
+            continue
+        if k == "timesteps" and isinstance(v, torch.Tensor):
+            v = v.tolist()
+        elif isinstance(v, torch.Tensor):
+            raise TypeError(f"SongParallelPipeline: tensor keyword {k!r} is neither conditioning nor a sampler "
+                            "argument; it cannot be split per song")
+        meta[k] = v
+    return meta
 
 
 class SongParallelPipeline:
@@ -290,9 +314,7 @@ class SongParallelPipeline:
             enc_nc, _, ctx_nc = be._non_cover_condition(kw, ctx)
             enc_nc, ctx_nc = enc_nc.to(dev, dtype), ctx_nc.to(dev, dtype)
         src = kw.get("src_latents") if float(kw.get("cover_noise_strength", 0.0)) > 0.0 else None
-        meta = {k: kw[k] for k in _SAMPLER_KW if k in kw}
-        if isinstance(meta.get("timesteps"), torch.Tensor):
-            meta["timesteps"] = meta["timesteps"].tolist()
+        meta = _rank_kwargs(kw)
         return self._run([enc, ctx, noise, None if src is None else src.to(dev, dtype), enc_nc, ctx_nc], meta)
 
     def serve_one(self) -> None:

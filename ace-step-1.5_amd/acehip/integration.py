@@ -134,10 +134,11 @@ def install(handler, max_seconds: float = 600.0, max_batch: int = 8, fallback: b
             det = AudioDetokenizer(ce.cfg, dev, max_patches=max_batch * patches)
             det.load({"detokenizer." + k: v for k, v in m.detokenizer.state_dict().items()})
         hip_prep = HipPrepareCondition(ce, fallback=m.prepare_condition, tokenizer=tok, detokenizer=det)
-        dit.prepare_condition = hip_prep
-        # the handler also calls prepare_condition itself before generate_audio
-        # (service_generate_execute.py:123-142); same contract, same HIP encoders
-        m.prepare_condition = hip_prep
+        # the handler calls prepare_condition itself (service_generate_execute.py:123-142) and then
+        # generate_audio calls it again on the same payload (base:1820): the handler's call records
+        # its outputs, generate_audio's consumes them — one encoder pass per request
+        dit.prepare_condition = hip_prep.consume
+        m.prepare_condition = hip_prep.record
         out_prep = hip_prep
     orig_generate = handler.model.generate_audio
 

@@ -96,13 +96,10 @@ struct SplitArgs {
     int units = 0; // attn_pw_kernel: > 0 = persistent over units [0, units) (no splits)
     // attn_fwd_kernel stream-K mode (sk_total > 0): the units' KV tiles form one sequence of
     // sk_total = units · sk_nt tiles (unit-major); workgroup c runs tiles
-    // [c·total/grid, (c+1)·total/grid) as pieces of at most a few units.  A piece that does not
-    // start at its unit's tile 0 is the first piece of its workgroup: it publishes its partial
-    // (O, m, l) as slab c (write-through stores) and then flags[c] = epoch; the piece holding
-    // tile 0 (its workgroup's LAST piece, so the later pieces were published long before) folds
-    // its own partial with slabs c+1, c+2, … in that order and writes O.
-    int sk_total = 0, sk_nt = 0, epoch = 0;
-    int *flags = nullptr;   // ≥ grid ints; monotonic epochs, never reset
+    // [c·total/grid, (c+1)·total/grid) as pieces of at most a few units.  A split unit's pieces
+    // meet through a last-arriver ticket (cnt[first workgroup], self-resetting) and slabs in ws
+    // (2·grid slots); no workgroup waits for another, so residency of the grid is not assumed.
+    int sk_total = 0, sk_nt = 0;
     int prio = 0;           // attn_fwd_kernel<2>: static s_setprio 1 for waves 4-7 (ACEHIP_ATTN_PRIO)
 };
 
@@ -289,7 +286,7 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
     // stream-K logical workgroup: the blocks of one XCD (bid ≡ x mod 8) take a contiguous range
     // of the tile sequence, so the units they walk share few K/V heads in that XCD's L2 (with
     // blockIdx.x itself, neighbouring ranges went to different XCDs: L2 hit rate 48 %,
-    // profiles/r05v_pmc_tcc.json); slabs and flags are indexed by the logical number
+    // profiles/r05v_pmc_tcc.json); slabs and tickets are indexed by the logical number
     const int cw = (streamk && ATT_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     if (streamk) {
         g0 = (int64_t)cw * sp.sk_total / gridDim.x;
@@ -655,41 +652,63 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
 
     bool write_o = true;
     if (streamk && !(pt0 == 0 && pt1 == sp.sk_nt)) {
+        // unit u is split over the pieces of workgroups c0 .. c1 (c0 holds tile 0).  No workgroup
+        // waits for another (nothing assumes the whole grid is resident: two ranks sharing a
+        // GPU, or a planned CU count above the device's, only delay pieces).  Ticket cnt[c0]:
+        // every later piece publishes its slab (slot c) and adds 1; the tile-0 piece adds BIG —
+        // if it sees all n later pieces already counted it folds at once from registers, else it
+        // publishes its own slab (slot grid + c0) and adds 1 more.  Whoever makes the count
+        // BIG + n + 1 (or the tile-0 piece seeing n) folds pieces c0, c0+1, …, c1 in that order
+        // with one expression (slab_fold), so O is the same bits whoever folds.
+        constexpr int BIG = 1 << 16;
         const int64_t wsz = 66 * 64;                   // floats per wave: 64 O + m + l per lane
+        const int G = (int)gridDim.x;
+        auto owner = [&](int64_t t) {                  // workgroup whose tile range holds tile t
+            int c = (int)(t * G / sp.sk_total);
+            while (c + 1 < G && ((int64_t)c + 1) * sp.sk_total / G <= t) ++c;
+            while (c > 0 && (int64_t)c * sp.sk_total / G > t) --c;
+            return c;
+        };
+        const int64_t ub = (int64_t)u * sp.sk_nt;
+        const int c0 = pt0 == 0 ? cw : owner(ub), c1 = owner(ub + sp.sk_nt - 1);
+        const int n = c1 - c0;
+        auto slot = [&](int c) { return sp.ws + ((int64_t)(c == c0 ? G + c0 : c) * 8 + wave) * wsz; };
+        __shared__ int s_fold;
         if (pt0 > 0) {
-            // a later piece of unit u (this workgroup's first piece): publish slab c, then the flag
-            slab_store(sp.ws + ((int64_t)cw * 8 + wave) * wsz, oacc, m, l, lane);
+            slab_store(slot(cw), oacc, m, l, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(sp.flags + cw, sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            write_o = false;
+            if (tid == 0) s_fold = atomicAdd(sp.cnt + c0, 1) == BIG + n;
+            __syncthreads();
         } else {
-            // the piece with tile 0 (this workgroup's last): fold the later pieces in order — the
-            // first pieces of workgroups c+1, c+2, … that start inside unit u
-            const int64_t uend = ((int64_t)u + 1) * sp.sk_nt;
-            for (int c2 = cw + 1; c2 < (int)gridDim.x; ++c2) {
-                if ((int64_t)c2 * sp.sk_total / gridDim.x >= uend) break;
-                __shared__ int s_ok;
-                if (tid == 0) {
-                    int ok = 0;
-                    for (int spin = 0; spin < (1 << 22); ++spin) {      // bounded: give up, never hang
-                        if (__hip_atomic_load(sp.flags + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sp.epoch) {
-                            ok = 1;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                    s_ok = ok;
-                }
+            if (tid == 0) s_fold = atomicAdd(sp.cnt + c0, BIG) == n;
+            __syncthreads();
+            if (!s_fold) {
+                slab_store(slot(cw), oacc, m, l, lane);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                f32x16 o2[4];
-                float m2, l2;
-                slab_load(sp.ws + ((int64_t)c2 * 8 + wave) * wsz, o2, m2, l2, lane);
-                if (!s_ok) m2 = __builtin_nanf("");      // timed out: poison the row rather than hang
-                slab_fold(oacc, m, l, o2, m2, l2, false);
+                if (tid == 0) s_fold = atomicAdd(sp.cnt + c0, 1) == BIG + n;
                 __syncthreads();
             }
         }
+        if (s_fold) {
+            const f32x16 own[4] = {oacc[0], oacc[1], oacc[2], oacc[3]};
+            const float m_own = m, l_own = l;
+            for (int c2 = c0; c2 <= c1; ++c2) {
+                if (c2 == cw) {                        // the folder's own partial: registers
+                    slab_fold(oacc, m, l, own, m_own, l_own, c2 == c0);
+                } else {
+                    f32x16 o2[4];
+                    float m2, l2;
+                    slab_load(slot(c2), o2, m2, l2, lane);
+                    slab_fold(oacc, m, l, o2, m2, l2, c2 == c0);
+                }
+            }
+            if (tid == 0) sp.cnt[c0] = 0;              // self-resetting for the next launch
+        } else {
+            write_o = false;
+        }
+        __syncthreads();                               // s_fold is reused by the next piece
     }
 
     if (write_o && qi < Sq) {                 // both lanes of a row pair (lane, lane ^ 32) agree
@@ -1712,16 +1731,8 @@ static int short_tpp() { return knobs().attn_short_tpp; }
 
 size_t attention_ws_bytes() {
     const size_t cus = std::max<size_t>(1024, (size_t)num_cus_attn());
-    // [tail-split tickets: cus ints][slabs: cus · 8 waves · 66·64 floats][stream-K flags: cus ints]
-    return cus * 8 * 66 * 64 * sizeof(float) + 2 * cus * sizeof(int);   // ≤ cus split parts in flight
-}
-
-// stream-K epochs: one per launch, process-wide, so a flag word never holds a value a later
-// launch could mistake for its own (the workspace is zeroed once at allocation)
-static int next_epoch() {
-    static std::atomic<int> e{0};
-    int v = e.fetch_add(1, std::memory_order_relaxed) + 1;
-    return v > 0 ? v : 1;
+    // [tickets: cus ints][slabs: cus · 8 waves · 66·64 floats]; stream-K uses 2 slabs per workgroup
+    return cus * 8 * 66 * 64 * sizeof(float) + cus * sizeof(int);   // ≤ cus split parts in flight
 }
 
 int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int B, int H, int KV,
@@ -1836,15 +1847,15 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // (384 units × 47 tiles on 256 CUs) 186.1 → 175.8 µs in one process; the one-round cross grid
     // (192 units × 11 tiles) loses, 34.8 → 45.8 (its pieces' restart + merge ≥ the 2.75 tiles
     // saved), so only grids of more units than CUs and long loops take it
+    // (two slab slots per workgroup: 2·cus ≤ the workspace's 1024 slots)
     if (kn.attn_streamk && ws && nrep == 2 && window < 0 && !kmask && units > cus && units % cus != 0 &&
-        unit_tiles >= 24) {
+        unit_tiles >= 24 && 2 * (size_t)cus <= (size_t)std::max(1024, cus)) {
         const size_t wcus = (size_t)std::max(1024, cus);
         sp = SplitArgs{nq, units, 1, nullptr, nullptr};
         sp.sk_nt = unit_tiles;
         sp.sk_total = units * unit_tiles;
-        sp.epoch = next_epoch();
+        sp.cnt = (int *)ws;
         sp.ws = (float *)((char *)ws + wcus * sizeof(int));
-        sp.flags = (int *)((char *)ws + wcus * sizeof(int) + wcus * 8 * 66 * 64 * sizeof(float));
         grid = cus;
     }
     sp.prio = kn.attn_prio;

@@ -24,6 +24,21 @@ def test_header_symbols_exported():
     assert lib.acehip_get_version() == 400 == _ffi.ABI_VERSION
 
 
+def test_library_built_from_this_tree(monkeypatch):
+    """acehip_build_hash() = the native-source hash of the sources beside the library, and the
+    binding refuses a library built from other sources (verdict r05 hygiene item)."""
+    from acehip import _ffi
+    lib = _ffi.lib()
+    assert _ffi.build_hash(lib) == _ffi.source_hash()
+    assert re.fullmatch(r"[0-9a-f]{16}", _ffi.build_hash(lib))
+    monkeypatch.setattr(_ffi, "_LIB", None)
+    monkeypatch.setattr(_ffi, "source_hash", lambda: "0" * 16)
+    with pytest.raises(RuntimeError, match="native sources"):
+        _ffi.lib()
+    monkeypatch.undo()
+    assert _ffi.lib() is lib
+
+
 def test_error_paths_without_gpu():
     from acehip import _ffi
     lib = _ffi.lib()

@@ -663,6 +663,36 @@ def test_forward_graph_replay_matches_eager(gpu_device):
     rt.close()
 
 
+def test_graph_replay_single_streamk_layer(gpu_device, monkeypatch):
+    """A captured forward whose body holds exactly ONE stream-K launch (advisor r05: with per-launch
+    epochs baked into the graph, each replay would have read the previous replay's flags as
+    already published).  Two layers (band, then full at S = 1600: 13 q-blocks × 2 rows = 26 units of
+    25 KV tiles on a 7-CU plan → stream-K), replayed several times: bit-identical to eager."""
+    from acehip.dit import DiTRuntime
+    set_knob(monkeypatch, "ACEHIP_ATTN_CUS", "7")
+    set_knob(monkeypatch, "ACEHIP_ATTN_STREAMK", "1")
+    cfg = DiTConfig.tiny(layers=2, window=8)
+    W = {k: v.to(gpu_device, torch.bfloat16) for k, v in synth_dit_weights(cfg, seed=5, mode="parity").items()}
+    g = torch.Generator().manual_seed(12)
+    rt = DiTRuntime(cfg, 0, max_S=1600, max_Bc=2, max_Lenc=24)
+    rt.load(W)
+    T = 3200
+    enc = torch.randn(2, 24, cfg.hidden_size, generator=g).bfloat16().to(gpu_device)
+    rt.set_condition(enc)
+    t = torch.tensor([0.5], dtype=torch.float32, device=gpu_device)
+    outs = []
+    for graph in (False, True, True, True):
+        xt = torch.randn(1, T, 64, generator=torch.Generator().manual_seed(3)).bfloat16().to(gpu_device)
+        ctx = torch.randn(1, T, 128, generator=torch.Generator().manual_seed(4)).bfloat16().to(gpu_device)
+        rt.use_graph(graph)
+        outs.append(rt.forward(xt, ctx, t).clone())
+        torch.cuda.synchronize()
+    rt.close()
+    assert torch.isfinite(outs[0].float()).all()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(125, 12288, 2048, EPI_SWIGLU), (128, 12288, 2048, EPI_SWIGLU),
                                        (77, 1024, 512, EPI_SWIGLU), (1, 12288, 2048, EPI_SWIGLU),
                                        (125, 2048, 6144, EPI_RES), (125, 4096, 2048, EPI_STORE),
@@ -945,13 +975,16 @@ def test_cross_kv_grouped_gemms(gpu_device, monkeypatch):
 
 
 @pytest.mark.parametrize("cus,B,H,KV,Sq,Sk", [(16, 2, 4, 2, 700, 1600), (20, 2, 4, 2, 700, 3100), (0, 2, 16, 8, 3000, 3000),
-                                              (0, 2, 16, 8, 7500, 7500), (7, 1, 4, 2, 1000, 1700), (3, 1, 2, 1, 450, 1600)])
+                                              (0, 2, 16, 8, 7500, 7500), (7, 1, 4, 2, 1000, 1700), (3, 1, 2, 1, 450, 1600),
+                                              (512, 2, 16, 8, 7500, 7500), (384, 2, 16, 8, 3000, 3000)])
 def test_attention_streamk(gpu_device, monkeypatch, cus, B, H, KV, Sq, Sk):
     """Stream-K rounds (ACEHIP_ATTN_STREAMK=1) for unmasked full / cross layers: the units' KV tiles
-    as one sequence split evenly over the workgroups; pieces past a unit's tile 0 publish their
-    partial (O, m, l) and the piece holding tile 0 folds them in order.  ACEHIP_ATTN_CUS shrinks the
-    grid so units span 2-3 workgroups; cus = 0 is the real 240 s full / cross shape.  vs fp32, and
-    bit-identical across launches (the epoch flags are never reset)."""
+    as one sequence split evenly over the workgroups; a split unit's pieces meet through a
+    last-arriver ticket and the folder folds them in workgroup order.  ACEHIP_ATTN_CUS shrinks the
+    grid so units span 2-3 workgroups; cus = 0 is the real 240 s full / cross shape; cus = 384 / 512
+    plan more workgroups than the device holds at once (advisor r05: the old flag spin needed the
+    whole grid resident) — no workgroup waits for another, so those must be exact too.  vs fp32,
+    and bit-identical across launches whichever piece folds."""
     if cus:
         set_knob(monkeypatch, "ACEHIP_ATTN_CUS", str(cus))
     set_knob(monkeypatch, "ACEHIP_ATTN_STREAMK", "1")

@@ -6,8 +6,10 @@ synthetic weights (no reference code runs: the stub's own ``generate_audio`` /
 The handler is driven the way the reference drives it:
   * ``handler.model.prepare_condition(...)`` as ``_execute_service_generate_diffusion``
     calls it (service_generate_execute.py:123-142), then
-  * ``handler.model.generate_audio(**kwargs)`` with exactly the kwargs dict of
-    ``_build_service_generate_kwargs`` (service_generate_execute.py:78-104), under
+  * ``handler.model.generate_audio(**kwargs)`` — both calls' kwargs rebuilt from
+    ``tests/golden/seam_calls.json``, which ``tools/record_seam.py`` recorded by running the
+    reference's own ``_build_service_generate_kwargs`` / ``_execute_service_generate_diffusion``
+    (service_generate_execute.py:62-196) against a recording model — under
     ``torch.inference_mode()`` (:121),
   * ``handler.tiled_decode(latents[B, 64, T])`` (generate_music_decode.py:164),
   * the LoRA lifecycle methods (handler/lora/lifecycle.py:164-289) followed by a
@@ -19,6 +21,7 @@ import pytest
 import torch
 
 from conftest import cosine, rel_l2
+from seam_spec import build_calls
 
 from acehip.config import DiTConfig, VAEConfig
 from acehip.weights import synth_condenc_weights, synth_dit_weights, synth_null_condition, synth_vae_weights
@@ -168,57 +171,6 @@ class StubHandler:
         return "ok"
 
 
-def _service_kwargs(dev, B, T):
-    """_build_service_generate_kwargs (service_generate_execute.py:78-102), synthetic payload."""
-    g = torch.Generator(device="cpu").manual_seed(17)
-    bf = torch.bfloat16
-    Lt, Ll = 12, 20
-    tmask = torch.ones(B, Lt, dtype=torch.long)
-    tmask[1, 9:] = 0
-    lmask = torch.ones(B, Ll, dtype=torch.long)
-    lmask[0, 15:] = 0
-    payload = {
-        "text_hidden_states": torch.randn(B, Lt, 1024, generator=g).to(dev, bf),
-        "text_attention_mask": tmask.to(dev),
-        "lyric_hidden_states": torch.randn(B, Ll, 1024, generator=g).to(dev, bf),
-        "lyric_attention_mask": lmask.to(dev),
-        "refer_audio_acoustic_hidden_states_packed": torch.randn(B, 750, 64, generator=g).to(dev, bf),
-        "refer_audio_order_mask": torch.arange(B, dtype=torch.long, device=dev),
-        "src_latents": torch.randn(B, T, 64, generator=g).to(dev, bf),
-        "chunk_mask": torch.ones(B, T, 64, dtype=bf, device=dev),
-        "is_covers": torch.zeros(B, dtype=torch.long, device=dev),
-        "non_cover_text_hidden_states": None, "non_cover_text_attention_masks": None,
-        "precomputed_lm_hints_25Hz": None,
-    }
-    silence = torch.randn(1, 2 * T, 64, generator=g).to(dev, bf)
-    kwargs = {
-        "text_hidden_states": payload["text_hidden_states"],
-        "text_attention_mask": payload["text_attention_mask"],
-        "lyric_hidden_states": payload["lyric_hidden_states"],
-        "lyric_attention_mask": payload["lyric_attention_mask"],
-        "refer_audio_acoustic_hidden_states_packed": payload["refer_audio_acoustic_hidden_states_packed"],
-        "refer_audio_order_mask": payload["refer_audio_order_mask"],
-        "src_latents": payload["src_latents"],
-        "chunk_masks": payload["chunk_mask"],
-        "is_covers": payload["is_covers"],
-        "silence_latent": silence,
-        "seed": [11, 12],
-        "non_cover_text_hidden_states": payload["non_cover_text_hidden_states"],
-        "non_cover_text_attention_mask": payload["non_cover_text_attention_masks"],
-        "precomputed_lm_hints_25Hz": payload["precomputed_lm_hints_25Hz"],
-        "audio_cover_strength": 1.0,
-        "cover_noise_strength": 0.0,
-        "infer_method": "ode",
-        "infer_steps": 4,
-        "diffusion_guidance_sale": 7.0,
-        "use_adg": False,
-        "cfg_interval_start": 0.0,
-        "cfg_interval_end": 1.0,
-        "shift": 3.0,
-    }
-    return payload, kwargs
-
-
 @pytest.fixture
 def installed(gpu_device):
     from acehip.integration import install
@@ -233,22 +185,21 @@ def test_install_drives_handler_calls(gpu_device, installed):
     from acehip.condition import ConditionEncoder, HipPrepareCondition
     from acehip.dit import AceStepDiTBackend, DiTRuntime
     h, out = installed
-    B, T = 2, 60
-    payload, kw = _service_kwargs(gpu_device, B, T)
+    # the calls the reference's own seam makes into self.model for one request, rebuilt from the
+    # spec tools/record_seam.py recorded by running service_generate_execute.py:62-196
+    payload, silence, calls = build_calls("base_seed_list", gpu_device, seed_param=[11, 12])
+    assert [m for m, _ in calls] == ["prepare_condition", "generate_audio"]
+    kw = calls[1][1]
+    B, T = payload["src_latents"].shape[:2]
     cfg = _cfg()
+    prep = out["prepare_condition"]
+    passes0 = prep.passes
     with torch.inference_mode():
-        # service_generate_execute.py:123-142
-        enc, enc_mask, ctx = h.model.prepare_condition(
-            text_hidden_states=payload["text_hidden_states"], text_attention_mask=payload["text_attention_mask"],
-            lyric_hidden_states=payload["lyric_hidden_states"], lyric_attention_mask=payload["lyric_attention_mask"],
-            refer_audio_acoustic_hidden_states_packed=payload["refer_audio_acoustic_hidden_states_packed"],
-            refer_audio_order_mask=payload["refer_audio_order_mask"], hidden_states=payload["src_latents"],
-            attention_mask=torch.ones(B, T, device=gpu_device, dtype=torch.bfloat16),
-            silence_latent=kw["silence_latent"], src_latents=payload["src_latents"],
-            chunk_masks=payload["chunk_mask"], is_covers=payload["is_covers"],
-            precomputed_lm_hints_25Hz=payload["precomputed_lm_hints_25Hz"])
-        res = h.model.generate_audio(**kw)                     # service_generate_execute.py:194
+        enc, enc_mask, ctx = h.model.prepare_condition(**calls[0][1])    # service_generate_execute.py:123
+        res = h.model.generate_audio(**kw)                               # service_generate_execute.py:194
     torch.cuda.synchronize()
+    # one encoder pass serves both calls (the reference runs it twice: :123 and base:1820)
+    assert prep.passes - passes0 == 1
     # conditioning = the oracle's AceStepConditionEncoder on the stub's weights
     cpu = {k: v.cpu() for k, v in kw.items() if isinstance(v, torch.Tensor)}
     with torch.no_grad():
