@@ -29,7 +29,7 @@ EXPORTS = [
     "acehip_vae_create", "acehip_vae_set_weight", "acehip_vae_finalize", "acehip_vae_decode",
     "acehip_vae_decode_blocks",
     "acehip_vae_encode", "acehip_vae_destroy", "acehip_vae_conv", "acehip_vae_resunit",
-    "acehip_wav_peak_normalize", "acehip_wav_postprocess",
+    "acehip_wav_peak_normalize", "acehip_wav_postprocess", "acehip_wav_postprocess_pcm16",
     "acehip_gemm_bf16", "acehip_gemm_bf16_ex", "acehip_attention_bf16",
     "acehip_rmsnorm_bf16", "acehip_gemm_headpost_bf16", "acehip_attention_masked_bf16",
     "acehip_enc_create", "acehip_enc_set_weight", "acehip_enc_finalize", "acehip_enc_embed",
@@ -97,6 +97,7 @@ def _declare(lib):
         "acehip_vae_resunit": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P]),
         "acehip_wav_peak_normalize": (c_int, [P, c_int, c_int64, P, P]),
         "acehip_wav_postprocess": (c_int, [P, c_int, c_int64, P, c_int, c_float, P]),
+        "acehip_wav_postprocess_pcm16": (c_int, [P, c_int, c_int, c_int64, P, c_int, c_float, P, P]),
         "acehip_gemm_bf16": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
         "acehip_gemm_bf16_ex": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, c_int,
                                         c_int, P]),

@@ -635,17 +635,14 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
         if (tid == 0) s_ticket = atomicAdd(sp.cnt + (u - sp.full), 1);
         __syncthreads();
         if (s_ticket != nsplit - 1) return;
-        const f32x16 own[4] = {oacc[0], oacc[1], oacc[2], oacc[3]};
-        const float m_own = m, l_own = l;
-        for (int p2 = 0; p2 < nsplit; ++p2) {
-            if (p2 == part) {
-                slab_fold(oacc, m, l, own, m_own, l_own, p2 == 0);
-            } else {
-                f32x16 o2[4];
-                float m2, l2;
-                slab_load(ws_u + ((int64_t)p2 * 8 + wave) * wsz, o2, m2, l2, lane);
-                slab_fold(oacc, m, l, o2, m2, l2, p2 == 0);
-            }
+        // every part, this one's too, from its slab (fp32 store / load is exact): no register
+        // copy of the own partial held across the loop (that copy had spilled ~140 VGPRs)
+        slab_load(ws_u + wave * wsz, oacc, m, l, lane);
+        for (int p2 = 1; p2 < nsplit; ++p2) {
+            f32x16 o2[4];
+            float m2, l2;
+            slab_load(ws_u + ((int64_t)p2 * 8 + wave) * wsz, o2, m2, l2, lane);
+            slab_fold(oacc, m, l, o2, m2, l2, false);
         }
         if (tid == 0) sp.cnt[u - sp.full] = 0;         // self-resetting for the next launch
     }
@@ -692,17 +689,15 @@ __global__ __launch_bounds__(256 * NREP, 3 - NREP) void attn_fwd_kernel(const bf
             }
         }
         if (s_fold) {
-            const f32x16 own[4] = {oacc[0], oacc[1], oacc[2], oacc[3]};
-            const float m_own = m, l_own = l;
-            for (int c2 = c0; c2 <= c1; ++c2) {
-                if (c2 == cw) {                        // the folder's own partial: registers
-                    slab_fold(oacc, m, l, own, m_own, l_own, c2 == c0);
-                } else {
-                    f32x16 o2[4];
-                    float m2, l2;
-                    slab_load(slot(c2), o2, m2, l2, lane);
-                    slab_fold(oacc, m, l, o2, m2, l2, c2 == c0);
-                }
+            // the fold starts from piece c0: the tile-0 piece's own registers when it folds (the
+            // usual case), else its slab; a later piece that folds reads its own partial back from
+            // the slab it published (exact) — no register copy held across the loop
+            if (cw != c0) slab_load(slot(c0), oacc, m, l, lane);
+            for (int c2 = c0 + 1; c2 <= c1; ++c2) {
+                f32x16 o2[4];
+                float m2, l2;
+                slab_load(slot(c2), o2, m2, l2, lane);
+                slab_fold(oacc, m, l, o2, m2, l2, false);
             }
             if (tid == 0) sp.cnt[c0] = 0;              // self-resetting for the next launch
         } else {

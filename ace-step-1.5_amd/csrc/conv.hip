@@ -1779,8 +1779,11 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const bf16_t *__restrict_
             }
         }
     }
-    out[t] = acc[0];
-    out[L + t] = acc[1];
+    // rounded through bf16: the reference decodes with a bf16 VAE (init_service_loader.py:132-134),
+    // so decode(z).sample is bf16 and the handler upcasts it (generate_music_decode.py:188-189);
+    // the fp32 output holds exactly those values
+    out[t] = rbf(acc[0]);
+    out[L + t] = rbf(acc[1]);
 }
 
 // Encoder first conv: channels-first audio [Cin≤2][N] → NLC [N][Cout] raw + snaked, k=7 pad 3, bias.

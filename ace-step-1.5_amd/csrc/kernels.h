@@ -239,6 +239,8 @@ int swiglu_f32(const float *g, const float *u, float *o, int64_t n, hipStream_t 
 // decode guard (when guard != 0) then normalize_audio (when target_amp > 0), see small.hip
 int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s, float target_amp = 0.f,
                        int guard = 1);
+int wav_postprocess_pcm16(float *wav, int B, int C, int64_t N, float *peak, hipStream_t s, float target_amp,
+                          int guard, short *pcm);
 int cast_f32_bf16(const float *src, bf16_t *dst, int64_t n, hipStream_t s);
 
 }  // namespace acehip

@@ -206,6 +206,65 @@ __global__ __launch_bounds__(256) void wav_scale_kernel(float4 *w, int64_t n4, c
     }
 }
 
+// The output leg's sample conversion fused into the scale pass: after (1)+(2) above, every
+// sample is written back (the fp32 tensor the reference returns, inference.py:711) AND packed as
+// interleaved PCM16 [N][C] — the frame layout a WAV / FLAC writer consumes (soundfile gets
+// [samples, channels], audio_utils.py:173,190) — q = rint(clamp(x, −1, 1) · 32767), libsndfile's
+// float → 16-bit conversion (normalised, round-to-nearest-even; identical to its unclipped
+// lrintf(x · 0x7FFF) for |x| ≤ 1, which normalize_audio guarantees).  One thread: 4 frames.
+template <int C>
+__global__ __launch_bounds__(256) void wav_scale_pcm16_kernel(float *w, int64_t N, const float *peak, int guard,
+                                                              float target, short *pcm) {
+    const int b = blockIdx.y;
+    const float pk = peak[b];
+    const bool div = guard && pk > 1.0f;
+    const float p2 = div ? 1.0f : pk;
+    const bool norm = target > 0.f && !(p2 < 1e-6f);
+    const float gain = (1.0f / p2) * target;
+    float *p = w + (int64_t)b * C * N;
+    short *q = pcm + (int64_t)b * C * N;
+    const int64_t n4 = N / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        float v[C][4];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const float4 x = ((const float4 *)(p + (int64_t)c * N))[i];
+            v[c][0] = x.x; v[c][1] = x.y; v[c][2] = x.z; v[c][3] = x.w;
+        }
+        if (div || norm) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (div) v[c][j] /= pk;
+                    if (norm) v[c][j] *= gain;
+                }
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                ((float4 *)(p + (int64_t)c * N))[i] = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
+        }
+        short o[4 * C];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                o[j * C + c] = (short)__builtin_rintf(fminf(fmaxf(v[c][j], -1.0f), 1.0f) * 32767.0f);
+        if constexpr (C == 2) {
+            uint4 u;
+            u.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+            u.y = (uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16);
+            u.z = (uint32_t)(uint16_t)o[4] | ((uint32_t)(uint16_t)o[5] << 16);
+            u.w = (uint32_t)(uint16_t)o[6] | ((uint32_t)(uint16_t)o[7] << 16);
+            ((uint4 *)q)[i] = u;
+        } else {
+            uint2 u;
+            u.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+            u.y = (uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16);
+            ((uint2 *)q)[i] = u;
+        }
+    }
+}
+
 // FSQ (vector_quantize_pytorch FSQ.bound / codes_to_indices, restated; see
 // oracle/condenc_oracle.py): fp32 math as the library forces (force_quantization_f32)
 __global__ void fsq_quantize_kernel(const bf16_t *z, int64_t ldz, int M, FsqLevels lv, bf16_t *codes, int64_t ldc,
@@ -268,6 +327,22 @@ int wav_peak_normalize(float *wav, int B, int64_t n, float *peak, hipStream_t s,
     wav_peak_kernel<<<dim3(gx, B), 256, 0, s>>>((const float4 *)wav, n4, (unsigned *)peak);
     HIP_TRY(hipGetLastError());
     wav_scale_kernel<<<dim3(gx, B), 256, 0, s>>>((float4 *)wav, n4, peak, guard, target_amp);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int wav_postprocess_pcm16(float *wav, int B, int C, int64_t N, float *peak, hipStream_t s, float target_amp,
+                          int guard, short *pcm) {
+    HIP_TRY(hipMemsetAsync(peak, 0, (size_t)B * sizeof(float), s));
+    const int64_t n4 = N / 4;
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, (C * n4 + 255) / 256);
+    wav_peak_kernel<<<dim3(gx, B), 256, 0, s>>>((const float4 *)wav, C * n4, (unsigned *)peak);
+    HIP_TRY(hipGetLastError());
+    const unsigned gp = (unsigned)std::min<int64_t>(1024, (n4 + 255) / 256);
+    if (C == 2)
+        wav_scale_pcm16_kernel<2><<<dim3(gp, B), 256, 0, s>>>(wav, N, peak, guard, target_amp, pcm);
+    else
+        wav_scale_pcm16_kernel<1><<<dim3(gp, B), 256, 0, s>>>(wav, N, peak, guard, target_amp, pcm);
     HIP_TRY(hipGetLastError());
     return 0;
 }

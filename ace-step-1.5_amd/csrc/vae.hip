@@ -686,4 +686,16 @@ int acehip_wav_postprocess(float *wav, int B, int64_t n, float *peak, int guard,
     return wav_peak_normalize(wav, B, n, peak, (hipStream_t)stream, target_amp, guard);
 }
 
+// the same pass pair with the sample conversion of the output leg fused in: wav fp32 [B][C][N]
+// (channels-first, updated in place as above) → pcm int16 [B][N][C] (interleaved frames), ready
+// for a WAV / FLAC writer after one device→host copy of half the fp32 bytes
+int acehip_wav_postprocess_pcm16(float *wav, int B, int C, int64_t N, float *peak, int guard, float target_amp,
+                                 int16_t *pcm, void *stream) {
+    if (!wav || !peak || !pcm || B <= 0 || N <= 0) return fail(ACEHIP_E_ARG, "wav_postprocess_pcm16: argument");
+    if (C != 1 && C != 2) return fail(ACEHIP_E_ARG, "wav_postprocess_pcm16: 1 or 2 channels");
+    if (N % 4) return fail(ACEHIP_E_ARG, "wav_postprocess_pcm16: samples per channel must be a multiple of 4");
+    if (!(target_amp >= 0.f)) return fail(ACEHIP_E_ARG, "wav_postprocess_pcm16: target_amp must be >= 0");
+    return wav_postprocess_pcm16(wav, B, C, N, peak, (hipStream_t)stream, target_amp, guard, (short *)pcm);
+}
+
 }  // extern "C"

@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="CPU ranks over gloo with a stand-in song: exercises the launcher / timing / "
                         "max-over-ranks / JSON path without a GPU")
+    p.add_argument("--no-output-leg", action="store_true",
+                   help="skip the post-decode output leg measurement (D->H, PCM16 conversion, WAV write)")
     p.add_argument("--no-config1", action="store_true",
                    help="skip the CPU run of BASELINE config 1 (10 s turbo, 8 steps, fp32, in full)")
     return p.parse_args()
@@ -108,6 +110,88 @@ def host_cpus():
     except OSError:
         pass
     return n, n_host, model
+
+
+def output_leg(pipe, song, dev, sec_per_song, n_songs=2):
+    """SURVEY §8f row 4, measured after the timed region on rank 0: what happens to each song after
+    the decode.  (a) the reference's host leg (inference.py:673-716, audio_utils.py:24-210): fp32
+    D→H, normalize_audio on the host, the [samples, channels] PCM16 conversion soundfile applies,
+    the file write; (b) acehip's leg run serially: guard + normalize + PCM16 pack fused on the GPU,
+    D→H of the frames into pinned memory, the write; (c) (b) overlapped with the next songs (the
+    AudioWriter: copy on a side stream, write on a host thread): songs/s with the leg against the
+    timed line.  Files are PCM16 WAV via the stdlib `wave` module (soundfile / the FLAC encoder are
+    not installed, so FLAC encoding itself is not timed)."""
+    import tempfile
+    from acehip.output import AudioWriter, postprocess_pcm16_, reference_host_leg, remove_quietly, write_wav_pcm16
+    wav = pipe.wav
+    B, C, N = wav.shape
+    d = tempfile.mkdtemp(prefix="acehip_out_")
+    paths = []
+    try:
+        ref = None
+        for i in range(2):                      # the second run: warm page cache, like a serving loop
+            p = os.path.join(d, f"ref{i}.wav")
+            paths.append(p)
+            r = reference_host_leg(wav[0], p)
+            r.pop("frames")
+            ref = r if ref is None or r["total_ms"] < ref["total_ms"] else ref
+        host = torch.empty(N * C, dtype=torch.int16, pin_memory=True)
+        best = None
+        for i in range(2):
+            w = wav[:1].clone()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pcm = postprocess_pcm16_(w, -1.0)
+            e1.record()
+            host.copy_(pcm.view(-1), non_blocking=True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            p = os.path.join(d, f"hip{i}.wav")
+            paths.append(p)
+            write_wav_pcm16(p, host.view(N, C), 48000, C)
+            t2 = time.perf_counter()
+            cur = {"gpu_pack_ms": e0.elapsed_time(e1), "pack_plus_d2h_ms": 1e3 * (t1 - t0), "write_ms": 1e3 * (t2 - t1),
+                   "total_ms": 1e3 * (t2 - t0)}
+            best = cur if best is None or cur["total_ms"] < best["total_ms"] else best
+        writer = AudioWriter(dev, N, channels=C, slots=2)
+        db, pipe.normalization_db = pipe.normalization_db, None    # the writer's fused pass normalizes
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        try:
+            for i in range(n_songs):
+                song(500 + i)
+                p = os.path.join(d, f"song{i}.wav")
+                paths.append(p)
+                writer.submit(pipe.wav, [p])
+            writer.flush()
+            torch.cuda.synchronize()
+            with_leg = (time.perf_counter() - t0) / n_songs
+        finally:
+            pipe.normalization_db = db
+            writer.close()
+    finally:
+        remove_quietly(paths)
+        try:
+            os.rmdir(d)
+        except OSError:
+            pass
+    return {
+        "samples_per_song": N * C,
+        "reference_host_leg_ms": {k: round(v, 2) for k, v in ref.items()},
+        "reference_host_bytes_d2h": N * C * 4,
+        "acehip_serial_leg_ms": {k: round(v, 3) for k, v in best.items()},
+        "acehip_bytes_d2h": N * C * 2,
+        "overlapped_s_per_song_with_leg": round(with_leg, 4),
+        "overlapped_exposed_ms_per_song": round((with_leg - sec_per_song) * 1e3, 1),
+        "note": "reference leg = fp32 D->H + host normalize_audio + [samples, channels] PCM16 conversion + "
+                "WAV write (host torch on this job's CPU quota); acehip leg = fused GPU guard/normalize/PCM16 "
+                "pack + pinned D->H of half the bytes + WAV write; overlapped = songs run back to back with the "
+                "leg of song k (side-stream copy, writer thread) under song k+1 — exposed = its s/song minus "
+                "the timed line's; FLAC encoding not timed (soundfile absent)",
+    }
 
 
 def cpu_baseline(W_gpu, cfg, vae_w, vcfg, T, lenc, Bc=2, n_steps=1):
@@ -485,6 +569,10 @@ def main():
         "kernels": kernels,
         "kernels_note": "per-launch averages (HIP events on the forward stream) from one extra untimed song; the timed region carries events only around the roofline kernel",
     }
+    if rank == 0 and world == 1 and vae is not None and not args.no_output_leg:
+        leg = output_leg(pipe, song, dev, sec_per_song)
+        out["output_ms_per_song"] = leg["acehip_serial_leg_ms"]["total_ms"]
+        out["output_leg"] = leg
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # a short song (10 s, 8 turbo steps) runs in full; longer ones
         # time one DiT step + one 64-frame VAE window and extrapolate

@@ -350,6 +350,13 @@ int acehip_wav_peak_normalize(float *wav, int B, int64_t n, float *peak, void *s
  * peak pass + one scale pass. */
 int acehip_wav_postprocess(float *wav, int B, int64_t n, float *peak, int guard, float target_amp,
                            void *stream);
+/* The postprocess pass pair above with the output leg's sample conversion fused in (audio_utils.py
+ * AudioSaver.save_audio → soundfile PCM_16, the default FLAC / WAV subtype): wav fp32 [B][C][N]
+ * (C = 1 or 2, N % 4 == 0) is updated in place exactly as acehip_wav_postprocess does, and every
+ * sample is also written to pcm int16 [B][N][C] (interleaved frames) as
+ * rint(clamp(x, -1, 1) * 32767).  Halves the device→host bytes of the leg. */
+int acehip_wav_postprocess_pcm16(float *wav, int B, int C, int64_t N, float *peak, int guard, float target_amp,
+                                 int16_t *pcm, void *stream);
 
 /* ------------------------------------------------------------ kernels ---- */
 /* Single-kernel entry points used by the parity tests and the profiler

@@ -134,7 +134,8 @@ def decode_bf16_storage(W: Dict[str, Tensor], cfg, z: Tensor) -> Tensor:
         for n, d in ((1, 1), (2, 3), (3, 9)):
             x = _res_unit_b(W, f"{p}.res_unit{n}", x, d)
     x = _snake_b(W, "decoder.snake1", x)
-    return F.conv1d(x, _wb(W, "decoder.conv2"), None, padding=3)
+    # the bf16 VAE's decode(z).sample is bf16 (upcast later by the handler, generate_music_decode.py:188)
+    return _rb(F.conv1d(x, _wb(W, "decoder.conv2"), None, padding=3))
 
 
 def encode_mean_bf16_storage(W: Dict[str, Tensor], cfg, wav: Tensor) -> Tensor:
