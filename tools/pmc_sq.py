@@ -33,7 +33,14 @@ def per_kernel(db):
                 "select kernel_name, grid_size, start, end from kernels"):
             dur[(_short(name), int(grid))].append((e - s) * 1e-9)
     except sqlite3.Error:
-        pass
+        # newer rocpd schemas: the dispatch times ride on the counter rows (one per dispatch)
+        seen = {}
+        for did, name, grid, s, e in cur.execute(
+                "select dispatch_id, kernel_name, grid_size, start, end from counters_collection"):
+            if s is not None and e is not None:
+                seen[did] = ((_short(name), int(grid)), (e - s) * 1e-9)
+        for k, d in seen.values():
+            dur[k].append(d)
     out = {}
     for k, cs in vals.items():
         row = {c: sum(v) / len(v) for c, v in cs.items()}
