@@ -61,8 +61,8 @@ int acehip_get_version(void);
  * library; a DiT handle re-captures its HIP graph after a reload. */
 int acehip_reload_knobs(void);
 const char *acehip_last_error(void);
-/* Content hash of the native sources the library was built from (csrc/*.hip, csrc/*.h,
- * include/*.h; ace-step-1.5_amd/csrc/native_hash.py).  acehip/_ffi.py refuses a library whose
+/* Content hash of the native sources the library was built from (the .hip and .h files under
+ * csrc/ and include/; ace-step-1.5_amd/csrc/native_hash.py).  acehip/_ffi.py refuses a library whose
  * hash differs from the sources beside it, so a shipped binary is provably the tree's. */
 const char *acehip_build_hash(void);
 
