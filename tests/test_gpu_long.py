@@ -156,6 +156,31 @@ def test_vae_decode_full_length_windows(gpu_device, vae_full, T):
         assert r <= VAE_WIN_TOL and c >= 0.995, (T, c0, r, c)
 
 
+@pytest.mark.parametrize("T,chunk", [(6000, 512), (1000, 256)])
+def test_vae_tiled_decode_replays_reference_windows(gpu_device, vae_full, T, chunk):
+    """The windows and kept ranges the reference's OWN tiled decode uses (vae_decode_chunks.py,
+    recorded by tools/record_vae_seam.py into tests/golden/vae_seam.json), decoded one by one on
+    the HIP decoder and stitched as the reference stitches them: bit-identical to acehip's single
+    untiled decode of the whole song — the replacement of `handler.tiled_decode` changes no sample."""
+    import json
+    import os
+    from conftest import GOLDEN
+    cfg, W, be = vae_full
+    case = next(c for c in json.load(open(os.path.join(GOLDEN, "vae_seam.json")))["cases"]
+                if c["T"] == T and c["chunk"] == chunk and not c["offload_wav_to_cpu"])
+    g = torch.Generator(device=gpu_device).manual_seed(T + chunk)
+    z = torch.randn(1, 64, T, device=gpu_device, generator=g).bfloat16()
+    wav = be.decode_tensor(z)
+    parts = []
+    for (w0, w1), (k0, k1) in zip(case["windows"], case["keep"]):
+        win = be.decode_tensor(z[:, :, w0:w1].contiguous())
+        parts.append(win[:, :, k0:k1].clone())
+    torch.cuda.synchronize()
+    tiled = torch.cat(parts, dim=-1)
+    assert tiled.shape == wav.shape
+    assert torch.equal(tiled, wav)
+
+
 def test_vae_encode_full_length_windows(gpu_device, vae_full):
     cfg, W, be = vae_full
     T, hop = 6000, cfg.hop_length

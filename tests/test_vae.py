@@ -1,6 +1,8 @@
 """Oobleck VAE: oracle structure checks (CPU) and HIP decode/encode parity vs
 the fp32 CPU oracle (GPU).  VAE parity is UNPINNED against the reference
 (diffusers AutoencoderOobleck is absent; see oracle/vae_oracle.py)."""
+import os
+
 import pytest
 import torch
 
@@ -30,6 +32,44 @@ def test_weight_norm_fusion_matches_torch():
         conv.parametrizations.weight.original0.copy_(g)
         conv.parametrizations.weight.original1.copy_(v)
     assert torch.allclose(vae_oracle.fuse_weight_norm(g, v), conv.weight, atol=1e-6)
+
+
+def test_weight_norm_fusion_matches_reference_converter():
+    """The oracle's weight-norm fusion against the reference's own converter
+    (acestep/models/mlx/vae_convert.py:19-34 `_fuse_weight_norm`, numpy; fixture recorded by
+    tools/record_vae_seam.py) on Conv1d and ConvTranspose1d shapes of the decoder: the converter
+    adds 1e-9 to the norm (torch weight_norm, the GPU reference's path, does not), which is below
+    fp32 resolution at these norms."""
+    from conftest import load_golden
+    t = load_golden("vae_weight_norm")
+    names = sorted({k.rsplit(".", 1)[0] for k in t})
+    assert len(names) == 6
+    for n in names:
+        got = vae_oracle.fuse_weight_norm(t[n + ".weight_g"], t[n + ".weight_v"])
+        assert got.shape == t[n + ".fused"].shape
+        assert torch.allclose(got, t[n + ".fused"], rtol=2e-6, atol=1e-9), n
+
+
+def test_reference_tiled_decode_fixture():
+    """The reference's own tiled decode (vae_decode_chunks.py:13-166), recorded with an indexing
+    stand-in VAE (tools/record_vae_seam.py): for every (T, chunk, overlap 64, GPU / offload path) the
+    stitched output is exactly the untiled sample sequence — the property acehip's untiled decode
+    relies on (tests/test_gpu_long.py replays the same windows through the HIP decoder)."""
+    import json
+    from conftest import GOLDEN
+    d = json.load(open(os.path.join(GOLDEN, "vae_seam.json")))
+    hop = d["hop"]
+    assert len(d["cases"]) == 40
+    for c in d["cases"]:
+        assert c["stitched_is_untiled"], (c["T"], c["chunk"], c["offload_wav_to_cpu"])
+        assert sum(k1 - k0 for k0, k1 in c["keep"]) == c["T"] * hop
+        pos = 0
+        for (w0, w1), (k0, k1) in zip(c["windows"], c["keep"]):
+            assert w0 * hop + k0 == pos and 0 <= k0 < k1 <= (w1 - w0) * hop
+            pos += k1 - k0
+    # 240 s at the reference's largest chunk: 16 windows, 1.32x the useful frames decoded
+    c = next(c for c in d["cases"] if c["T"] == 6000 and c["chunk"] == 512 and not c["offload_wav_to_cpu"])
+    assert len(c["windows"]) == 16 and c["decoded_frames"] == 7920
 
 
 def test_tiny_decoder_runs_on_cpu():
