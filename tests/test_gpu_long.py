@@ -181,6 +181,31 @@ def test_vae_tiled_decode_replays_reference_windows(gpu_device, vae_full, T, chu
     assert torch.equal(tiled, wav)
 
 
+def test_vae_tiled_encode_replays_reference_windows(gpu_device, vae_full):
+    """The reference's own tiled encode (vae_encode_chunks.py:10-98, 30 s chunks, 2 s overlap,
+    recorded by tools/record_vae_seam.py) replayed on the HIP encoder at 240 s: the stitched means
+    (latent_dist.mode(); the reference's per-chunk Gaussian draw is unseeded) are bit-identical to
+    acehip's single untiled encode — the replacement of `handler.tiled_encode` changes no mean."""
+    import json
+    import os
+    from conftest import GOLDEN
+    cfg, W, be = vae_full
+    case = next(c for c in json.load(open(os.path.join(GOLDEN, "vae_seam.json")))["encode_cases"]
+                if c["T"] == 6000 and c["chunk"] == 48000 * 30 and not c["offload_latent_to_cpu"])
+    N = 6000 * cfg.hop_length
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    x = (0.3 * torch.randn(1, 2, N, device=gpu_device, generator=g)).bfloat16()
+    full = be.encode_tensor(x, sample=False)
+    parts = []
+    for (s0, s1), (k0, k1) in zip(case["windows"], case["keep"]):
+        z = be.encode_tensor(x[:, :, s0:s1].contiguous(), sample=False)
+        parts.append(z[:, :, k0:k1].clone())
+    torch.cuda.synchronize()
+    tiled = torch.cat(parts, dim=-1)
+    assert tiled.shape == full.shape == (1, 64, 6000)
+    assert torch.equal(tiled, full)
+
+
 def test_vae_encode_full_length_windows(gpu_device, vae_full):
     cfg, W, be = vae_full
     T, hop = 6000, cfg.hop_length

@@ -67,6 +67,9 @@ def test_reference_tiled_decode_fixture():
         for (w0, w1), (k0, k1) in zip(c["windows"], c["keep"]):
             assert w0 * hop + k0 == pos and 0 <= k0 < k1 <= (w1 - w0) * hop
             pos += k1 - k0
+    for c in d["encode_cases"]:
+        assert c["stitched_is_untiled"], (c["T"], c["chunk"], c["offload_latent_to_cpu"])
+        assert sum(k1 - k0 for k0, k1 in c["keep"]) == c["T"]
     # 240 s at the reference's largest chunk: 16 windows, 1.32x the useful frames decoded
     c = next(c for c in d["cases"] if c["T"] == 6000 and c["chunk"] == 512 and not c["offload_wav_to_cpu"])
     assert len(c["windows"]) == 16 and c["decoded_frames"] == 7920

@@ -107,6 +107,60 @@ def record_tiling():
     return out
 
 
+class IndexEncVae:
+    """encode(x).latent_dist.sample() for audio [1, 2, N] whose channel 0 holds the global sample
+    index: latents [1, 64, N // 1920] tagged (call number)·2³² + (frame index within the window)."""
+
+    def __init__(self):
+        self.calls = []
+        self.dtype = torch.float64
+
+    def encode(self, x):
+        s0, N = int(x[0, 0, 0].item()), x.shape[-1]
+        n = len(self.calls)
+        self.calls.append((s0, s0 + N))
+        lat = n * TAG + torch.arange(N // HOP, dtype=torch.float64)
+        return types.SimpleNamespace(latent_dist=types.SimpleNamespace(
+            sample=lambda: lat.view(1, 1, -1).repeat(1, 64, 1)))
+
+
+def record_encode_tiling():
+    """vae_encode_chunks.py:10-98 (chunks of 30 s / 15 s, overlap 2 s, both paths)."""
+    mod = _load(os.path.join(REF, "core/generation/handler/vae_encode_chunks.py"), "_ref_vae_encode_chunks")
+
+    class Host(mod.VaeEncodeChunksMixin):
+        def __init__(self):
+            self.vae = IndexEncVae()
+            self.disable_tqdm = True
+            self.device = "cpu"
+
+    out = []
+    for T in (1500, 6000, 15000):
+        N = T * HOP
+        for chunk in (48000 * 30, 48000 * 15):
+            overlap = 48000 * 2
+            for offload in (False, True):
+                h = Host()
+                x = torch.zeros(1, 2, N, dtype=torch.float64)
+                x[0, 0] = torch.arange(N, dtype=torch.float64)
+                stride = chunk - 2 * overlap
+                steps = -(-N // stride)
+                fn = h._tiled_encode_offload_cpu if offload else h._tiled_encode_gpu
+                lat = fn(x, 1, N, stride, overlap, steps, chunk)[0, 0]
+                wid = torch.floor(lat / TAG)
+                local = lat - wid * TAG
+                starts = torch.tensor([c[0] // HOP for c in h.vae.calls], dtype=torch.float64)
+                exact = lat.numel() == T and bool(torch.equal(starts[wid.long()] + local,
+                                                              torch.arange(T, dtype=torch.float64)))
+                keep = []
+                for n in range(len(h.vae.calls)):
+                    sel = local[wid == n]
+                    keep.append([int(sel.min().item()), int(sel.max().item()) + 1] if sel.numel() else [0, 0])
+                out.append({"T": T, "chunk": chunk, "overlap": overlap, "offload_latent_to_cpu": offload,
+                            "windows": [list(c) for c in h.vae.calls], "keep": keep, "stitched_is_untiled": exact})
+    return out
+
+
 def record_weight_norm():
     mod = _load(os.path.join(REF, "models/mlx/vae_convert.py"), "_ref_vae_convert")
     rng = np.random.Generator(np.random.PCG64(7))
@@ -129,9 +183,13 @@ def record_weight_norm():
 def main():
     os.makedirs(OUT, exist_ok=True)
     tiling = record_tiling()
+    enc = record_encode_tiling()
     with open(os.path.join(OUT, "vae_seam.json"), "w") as f:
         json.dump({"reference": "acestep/core/generation/handler/vae_decode_chunks.py:13-166",
-                   "generator": "tools/record_vae_seam.py", "hop": HOP, "cases": tiling}, f)
+                   "generator": "tools/record_vae_seam.py", "hop": HOP, "cases": tiling,
+                   "encode_reference": "acestep/core/generation/handler/vae_encode_chunks.py:10-98",
+                   "encode_cases": enc}, f)
+    print("encode cases", len(enc), "not exact", sum(not c["stitched_is_untiled"] for c in enc))
     save_file(record_weight_norm(), os.path.join(OUT, "vae_weight_norm.safetensors"),
               metadata={"reference": "acestep/models/mlx/vae_convert.py:19-34 (_fuse_weight_norm)",
                         "generator": "tools/record_vae_seam.py"})
