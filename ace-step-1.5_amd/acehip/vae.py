@@ -68,7 +68,8 @@ class OobleckBackend:
         check(lib().acehip_vae_decode(self.h, ptr(z), B, T, ptr(out), stream_ptr()), "vae_decode")
         return out
 
-    def peak_normalize_(self, wav: torch.Tensor) -> torch.Tensor:
+    @staticmethod
+    def peak_normalize_(wav: torch.Tensor) -> torch.Tensor:
         """In place: songs whose peak |x| exceeds 1 are divided by it — the decode
         output guard of ``_decode_generate_music_pred_latents``
         (generate_music_decode.py:190-192).  wav fp32 [B, C, N] on the device."""
@@ -79,7 +80,8 @@ class OobleckBackend:
               "wav_peak_normalize")
         return wav
 
-    def postprocess_(self, wav: torch.Tensor, normalization_db: Optional[float] = -1.0) -> torch.Tensor:
+    @staticmethod
+    def postprocess_(wav: torch.Tensor, normalization_db: Optional[float] = -1.0) -> torch.Tensor:
         """In place, one fused HIP pass pair per batch: the decode guard (divide a song by
         its peak when > 1, generate_music_decode.py:193-195) followed by the product's
         ``normalize_audio(audio, normalization_db)`` (audio_utils.py:24-62, applied at

@@ -194,6 +194,25 @@ def test_vae_two_handles_alternate(gpu_device):
 
 
 @pytest.mark.gpu
+def test_decode_guard_vs_reference_function(gpu_device):
+    """The peak guard against the reference's own `_decode_generate_music_pred_latents`
+    (generate_music_decode.py:98-201), recorded by tools/record_vae_seam.py with a stand-in bf16
+    VAE: songs with a peak above 1, below 1, near silence and exactly 1 — bit-exact, through both
+    product entry points (the guard alone and the guard + normalize pass with normalization off)."""
+    from conftest import load_golden
+    from acehip.vae import OobleckBackend
+    t = load_golden("decode_guard")
+    x = t["wav_bf16"].float().to(gpu_device).contiguous()      # the handler's .float() (:188-189)
+    a = x.clone()
+    OobleckBackend.peak_normalize_(a)
+    b = x.clone()
+    OobleckBackend.postprocess_(b, normalization_db=None)
+    torch.cuda.synchronize()
+    assert torch.equal(a.cpu(), t["pred_wavs"])
+    assert torch.equal(b.cpu(), t["pred_wavs"])
+
+
+@pytest.mark.gpu
 def test_wav_peak_normalize(gpu_device):
     """generate_music_decode.py:190-192 output guard, bit-exact vs the torch formula."""
     from acehip.vae import OobleckBackend
@@ -237,6 +256,29 @@ def test_wav_postprocess_guard_plus_normalize(gpu_device, db):
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ref)
     be.close()
+
+
+def test_normalize_audio_oracle_vs_reference_function():
+    """oracle.audio_oracle.normalize_audio against the reference's own normalize_audio
+    (audio_utils.py:24-62), recorded by tools/record_vae_seam.py: bit-exact."""
+    from conftest import load_golden
+    from oracle import audio_oracle
+    t = load_golden("normalize_audio")
+    for i in range(5):
+        out = audio_oracle.normalize_audio(t[f"case{i}.in"], float(t[f"case{i}.db"][0]))
+        assert torch.equal(out, t[f"case{i}.out"]), i
+
+
+@pytest.mark.gpu
+def test_hip_normalize_audio_vs_reference_fixture(gpu_device):
+    """integration.hip_normalize_audio against the reference function's recorded outputs."""
+    from conftest import load_golden
+    from acehip.integration import hip_normalize_audio
+    t = load_golden("normalize_audio")
+    for i in range(5):
+        out = hip_normalize_audio(t[f"case{i}.in"].to(gpu_device), float(t[f"case{i}.db"][0]))
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), t[f"case{i}.out"]), i
 
 
 @pytest.mark.gpu

@@ -17,7 +17,14 @@ the reference never travels):
    tensors: inputs and fused outputs, against which ``tests/test_vae.py`` checks the oracle's
    ``fuse_weight_norm``.
 
-Writes ``tests/golden/vae_seam.json`` and ``tests/golden/vae_weight_norm.safetensors``."""
+3. The decode output guard (``generate_music_decode.py:98-201``
+   ``_decode_generate_music_pred_latents``, ``acestep.gpu_config`` stubbed) with a stand-in bf16 VAE:
+   the waveform it returns and the guarded fp32 ``pred_wavs`` the reference hands on.
+
+4. ``normalize_audio`` (``acestep/audio_utils.py:24-62``, torchaudio stubbed) on seeded songs.
+
+Writes ``tests/golden/vae_seam.json``, ``vae_weight_norm.safetensors``, ``decode_guard.safetensors``
+and ``normalize_audio.safetensors``."""
 from __future__ import annotations
 
 import importlib.util
@@ -161,6 +168,78 @@ def record_encode_tiling():
     return out
 
 
+def record_decode_guard():
+    """generate_music_decode.py:98-201 `_decode_generate_music_pred_latents` (loguru and
+    acestep.gpu_config stubbed) with a stand-in bf16 VAE returning a fixed waveform per song:
+    the input waveform and the guarded fp32 `pred_wavs` the reference hands on."""
+    if "acestep.gpu_config" not in sys.modules:
+        for name in ("acestep", "acestep.gpu_config"):
+            sys.modules.setdefault(name, types.ModuleType(name))
+        sys.modules["acestep.gpu_config"].get_effective_free_vram_gb = lambda: 100.0
+    mod = _load(os.path.join(REF, "core/generation/handler/generate_music_decode.py"), "_ref_generate_music_decode")
+    g = torch.Generator().manual_seed(11)
+    T = 4
+    wav = torch.randn(4, 2, T * HOP, generator=g)
+    wav[0] *= 2.5                                   # peak > 1: divided by its peak
+    wav[1] *= 0.2                                   # below 1: untouched
+    wav[2] *= 1e-6                                  # near silence
+    wav[3] = wav[3] / wav[3].abs().max()            # exactly 1 after the bf16 cast? (kept as is)
+    wav = wav.bfloat16()
+
+    class StandInVae:
+        dtype = torch.bfloat16
+
+        def decode(self, z):
+            assert z.dtype == torch.bfloat16 and z.shape == (4, 64, T)
+            return types.SimpleNamespace(sample=wav.clone())
+
+        def parameters(self):
+            return iter([torch.zeros(1)])
+
+    import contextlib
+
+    class Host(mod.GenerateMusicDecodeMixin):
+        def __init__(self):
+            self.vae = StandInVae()
+            self.device = "cpu"
+            self.use_mlx_vae = False
+            self.mlx_vae = None
+            self.current_offload_cost = 0.0
+
+        @contextlib.contextmanager
+        def _load_model_context(self, name):
+            yield
+
+        def _empty_cache(self):
+            pass
+
+        def _memory_allocated(self):
+            return 0
+
+        def _max_memory_allocated(self):
+            return 0
+
+    lat = torch.randn(4, T, 64, generator=g).bfloat16()
+    out, lat_cpu, _ = Host()._decode_generate_music_pred_latents(lat, None, False, {"total_time_cost": 0.0})
+    assert out.dtype == torch.float32
+    return {"wav_bf16": wav, "pred_wavs": out.contiguous()}
+
+
+def record_normalize_audio():
+    """acestep/audio_utils.py:24-62 `normalize_audio` (torchaudio stubbed: only AudioSaver uses it)
+    on seeded songs of several loudness levels and target dB: inputs and outputs."""
+    sys.modules.setdefault("torchaudio", types.ModuleType("torchaudio"))
+    mod = _load(os.path.join(REF, "audio_utils.py"), "_ref_audio_utils")
+    g = torch.Generator().manual_seed(5)
+    t = {}
+    for i, (scale, db) in enumerate([(3.0, -1.0), (0.3, -1.0), (1e-8, -1.0), (0.7, -6.0), (0.05, 0.0)]):
+        a = torch.randn(2, 48000, generator=g) * scale
+        t[f"case{i}.in"] = a
+        t[f"case{i}.db"] = torch.tensor([db])
+        t[f"case{i}.out"] = mod.normalize_audio(a, db).clone()   # silence comes back as the input object
+    return t
+
+
 def record_weight_norm():
     mod = _load(os.path.join(REF, "models/mlx/vae_convert.py"), "_ref_vae_convert")
     rng = np.random.Generator(np.random.PCG64(7))
@@ -192,6 +271,12 @@ def main():
     print("encode cases", len(enc), "not exact", sum(not c["stitched_is_untiled"] for c in enc))
     save_file(record_weight_norm(), os.path.join(OUT, "vae_weight_norm.safetensors"),
               metadata={"reference": "acestep/models/mlx/vae_convert.py:19-34 (_fuse_weight_norm)",
+                        "generator": "tools/record_vae_seam.py"})
+    save_file(record_decode_guard(), os.path.join(OUT, "decode_guard.safetensors"),
+              metadata={"reference": "acestep/core/generation/handler/generate_music_decode.py:98-201",
+                        "generator": "tools/record_vae_seam.py"})
+    save_file(record_normalize_audio(), os.path.join(OUT, "normalize_audio.safetensors"),
+              metadata={"reference": "acestep/audio_utils.py:24-62 (normalize_audio)",
                         "generator": "tools/record_vae_seam.py"})
     bad = [c for c in tiling if not c["stitched_is_untiled"]]
     print(f"wrote {len(tiling)} tiling cases ({len(bad)} not exact) and the weight-norm fixture")
