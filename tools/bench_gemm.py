@@ -8,7 +8,10 @@ from acehip import _ffi as ff
 
 dev = torch.device("cuda:0")
 shapes = {"swiglu": (6000, 12288, 2048), "down": (6000, 2048, 6144), "qkv": (6000, 4096, 2048),
-          "o": (6000, 2048, 2048), "o_half": (3000, 2048, 2048), "qkv_half": (3000, 4096, 2048), "crossq": (3000, 2048, 2048), "eq_k6144": (8192, 2048, 6144), "eq_k2048": (8192, 2048, 2048), "vae_k7_c128": (46080, 128, 896), "vae_k7_c512": (360000 // 4, 512, 3584)}
+          "o": (6000, 2048, 2048), "o_half": (3000, 2048, 2048), "qkv_half": (3000, 4096, 2048), "crossq": (3000, 2048, 2048), "eq_k6144": (8192, 2048, 6144), "eq_k2048": (8192, 2048, 2048), "vae_k7_c128": (46080, 128, 896), "vae_k7_c512": (360000 // 4, 512, 3584),
+          # stream-K what-if probes: one round of 256² tiles at a given K-tile count
+          "r256_k2048": (4096, 4096, 2048), "r128_k1024": (2048, 4096, 1024), "r256_k4608": (4096, 4096, 4608),
+          "r256_k1536": (4096, 4096, 1536)}
 variants = [int(v) for v in os.environ.get("VARIANTS", "0,4,6,7,8").split(",")]
 # COLD=1: rotate through enough weight copies (> 512 MB) that W comes from HBM
 # every launch, as in the DiT forward (1.2 GB of weights per step, MALL 256 MB)
