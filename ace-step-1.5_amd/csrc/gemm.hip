@@ -504,7 +504,7 @@ __device__ __forceinline__ void headpost_epilogue(const GemmArgs &a, char *lds, 
     const bool norm = head < nqk;
     const bool rope = h.cos != nullptr;
     const int r0 = wave * RPW + (HPT == 2 ? sub >> 1 : sub);
-    const int mf = min(m0 + r0, a.M - 1);
+    const int mf = min(m0 + r0, a.M - 1) + h.m_off;
     const int b0 = mf / h.S, s0 = mf - b0 * h.S;
     uint4 cv[ITER], sv[ITER];
     if (rope) {
@@ -710,7 +710,24 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs &a, char *lds, int b
     if (wr == 0) bar();   // balance the barrier count
     GSTAMP(2);
 
-    if constexpr (EPI == EPI_HEADPOST) {
+    if constexpr (EPI == EPI_HEADPOST && BM == 256) {
+        // the 256-row staging tile (135 KB at the padded pitch) exceeds the operand ring: the two
+        // wave groups' 128-row halves go through it one after the other (headpost_epilogue's
+        // opening barrier keeps half 1's staging behind half 0's row pass)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+            headpost_epilogue<128, 8, 2 * BUF, 2>(a, lds, m0 + hf * 128, n0, wave, lane, [&](bf16_t *st, int pitch) {
+                if (wr != hf) return;
+#pragma unroll
+                for (int i = 0; i < SM; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                        *(uint2 *)(st + (i * 16 + fr) * pitch + wc * 64 + j * 16 + fc * 4) = pack4(o);
+                    }
+            });
+        return;
+    } else if constexpr (EPI == EPI_HEADPOST) {
         headpost_epilogue<BM, 8, 2 * BUF, 2>(a, lds, m0, n0, wave, lane, [&](bf16_t *st, int pitch) {
 #pragma unroll
             for (int i = 0; i < SM; ++i)
@@ -984,11 +1001,11 @@ int launch_pp(const GemmArgs &a, hipStream_t s) {
             }
             return fail(-1, "gemm: the conv epilogue runs on the 256- or 128-row ping-pong tile");
         case EPI_HEADPOST:
-            if constexpr (BM == 192 || BM == 128) {
+            if constexpr (BM == 256 || BM == 192 || BM == 128) {
                 gemm_pp_kernel<BM, EPI_HEADPOST><<<tiles, 512, 0, s>>>(a);
                 break;
             }
-            return fail(-1, "gemm: head-post epilogue needs the 192- or 128-row ping-pong tile");
+            return fail(-1, "gemm: head-post epilogue needs the 256-, 192- or 128-row ping-pong tile");
         default: return fail(-1, "gemm: bad epilogue");
     }
     HIP_TRY(hipGetLastError());
@@ -1186,7 +1203,7 @@ static int splitk_finish(const GemmArgs &a, const GemmArgs &p, int splits, hipSt
 // epilogues only (store / SwiGLU; the gated residual indexes its batch by row).
 // ACEHIP_GEMM_TAILSPLIT=0 disables it.  Returns 1 when not applicable.
 static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
-    if (a.epi != EPI_SWIGLU && a.epi != EPI_STORE) return 1;
+    if (a.epi != EPI_SWIGLU && a.epi != EPI_STORE && a.epi != EPI_HEADPOST) return 1;
     if (!knobs().gemm_tailsplit) return 1;
     const int BMv = v == 7 ? 256 : 192, cus = num_cus();   // v = 7 or 8
     const int64_t nN = a.N / 256, tiles = (int64_t)((a.M + BMv - 1) / BMv) * nN;
@@ -1200,15 +1217,18 @@ static int gemm_tail_split(const GemmArgs &a, int v, hipStream_t s) {
     GemmArgs tl = a;
     tl.M = a.M - (int)M1;
     tl.A = a.A + M1 * a.lda;
-    tl.C = a.C + M1 * a.ldc;
+    if (a.epi == EPI_HEADPOST) tl.hp.m_off += (int)M1;   // C unused: rows scatter by (b, s)
+    else tl.C = a.C + M1 * a.ldc;
     // ACEHIP_GEMM_TAIL=1: the tail as one round of 128×256 two-phase ping-pong tiles
     const bool pp128 = knobs().gemm_tail == 1 && a.N % 256 == 0 && ((tl.M + 127) / 128) * nN <= cus;
+    if (a.epi == EPI_HEADPOST && !pp128) return 1;   // the 128×128 tail tile has no head-post epilogue
     if (pp128 && v == 7 && knobs().gemm_tailfuse) {
         // both grids in one launch (the main grid's block count is a multiple of 8, so the tail
         // blocks' XCD is their own index mod 8, as in a launch of their own)
         const int nmain = (int)(full * cus / nN * nN), ntail = ((tl.M + 127) / 128) * (int)nN;
         if (nmain % 8 == 0 && nmain == (hd.M / 256) * (int)nN && hd.M % 256 == 0) {
             if (a.epi == EPI_SWIGLU) klaunch(gemm_pp_split_kernel<EPI_SWIGLU>, dim3(nmain + ntail), dim3(512), s, hd, tl, nmain);
+            else if (a.epi == EPI_HEADPOST) gemm_pp_split_kernel<EPI_HEADPOST><<<nmain + ntail, 512, 0, s>>>(hd, tl, nmain);
             else gemm_pp_split_kernel<EPI_STORE><<<nmain + ntail, 512, 0, s>>>(hd, tl, nmain);
             HIP_TRY(hipGetLastError());
             return 0;
@@ -1301,6 +1321,18 @@ int gemm(const GemmArgs &a, hipStream_t s, RowAdd *defer) {
             hh.src = st.C;
             hh.ld_src = a.N;
             return head_post(hh, s);
+        }
+        // whole rounds of 256-row tiles + one round of 128-row tiles where that costs less than
+        // the 192-row rounds (cost model of gemm_pick_variant, a 128×256 tile ≈ 0.6 of a 192×256
+        // one): QKV at 240 s, 32 × 16 = 2 rounds of 192 → 1 round of 256 + 1 of 128
+        if (kn.gemm_hp_tail && a.N % 256 == 0) {
+            const int cus = num_cus();
+            const int64_t nN = a.N / 256, t7 = ((a.M + 255) / 256) * nN, t8 = ((a.M + 191) / 192) * nN;
+            const double c_split = (double)(t7 / cus) * 1.093 + 0.6, c8 = (double)((t8 + cus - 1) / cus);
+            if (t7 >= cus && c_split < c8) {
+                const int rc = gemm_tail_split(a, 7, s);
+                if (rc <= 0) return rc;
+            }
         }
         return gemm_variant(a, 8, s);
     }

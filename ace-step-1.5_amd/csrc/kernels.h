@@ -30,6 +30,7 @@ struct Knobs {
     int attn_prio = 0;        // ACEHIP_ATTN_PRIO: attn_fwd_kernel<2> waves 4-7 at s_setprio 1 (the guide's static priority)
     int gemm_pp128 = 1;       // ACEHIP_GEMM_PP128: a one-round 192-row grid whose 128-row grid also fits one round runs on 128-row tiles
     int gemm_tailfuse = 1;    // ACEHIP_GEMM_TAILFUSE: the tail-split GEMM's main and tail grids in one launch
+    int gemm_hp_tail = 1;     // ACEHIP_GEMM_HPTAIL: head-post GEMMs as a tail split (256-row main rounds + a 128-row tail round) where the cost model prefers it
     int convt = 1;            // ACEHIP_CONVT: 1 ConvTranspose (N % 256 == 0, padded input) as an implicit GEMM, 0 conv_gemm_kernel
     int conv7 = 2;            // ACEHIP_CONV7: k = 7 VAE convs — 2 implicit GEMM on the ping-pong tile (C ≥ 256, padded input), 1 halo-staged conv7_kernel
     int conv_bm128 = 2;       // ACEHIP_CONV_BM128: GEMM convs whose 256-row grid fills ≤ 1/2 of the chip on 128-row tiles, ≤ 1/4 on 64-row (2; 1: 128 only; 0: 256 always)
@@ -55,6 +56,7 @@ struct HeadPostArgs {
     // split-K input (gemm's small-M path): the projection is Σ_s part[s·plane + row·ld_src + col]
     // (fp32 partials summed in split order, then rounded to bf16) instead of src
     const float *part = nullptr; int splits = 0; int64_t plane = 0;
+    int m_off = 0;                       // row of the full projection that GEMM row 0 is (tail-split grids)
 };
 enum GemmEpi {
     EPI_STORE = 0,       // C = bf16(acc + bias)

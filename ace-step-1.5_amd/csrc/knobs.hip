@@ -41,6 +41,7 @@ Knobs read_env() {
     k.conv7 = env_int("ACEHIP_CONV7", 2);
     k.convt = env_int("ACEHIP_CONVT", 1);
     k.gemm_tailfuse = env_int("ACEHIP_GEMM_TAILFUSE", 1);
+    k.gemm_hp_tail = env_int("ACEHIP_GEMM_HPTAIL", 1);
     k.gemm_pp128 = env_int("ACEHIP_GEMM_PP128", 1);
     k.attn_prio = env_int("ACEHIP_ATTN_PRIO", 0);
     k.convp = env_int("ACEHIP_CONVP", 3);

@@ -47,6 +47,7 @@ def _headpost_ref(C, B, S, nq, nk, nv, qw, kw, cos, sin, eps):
     (1, 125, 16, 8, 8, 2048, True),    # short song: split-K partials + standalone head_post
     (1, 3000, 16, 0, 0, 2048, False),  # cross-Q of the cond rows: half-chip grid → 192×128 one-head tiles
     (1, 2990, 8, 4, 4, 256, True),     # same tile choice with k / v heads, RoPE and a ragged last tile
+    (2, 3000, 16, 8, 8, 256, True),    # the 240 s QKV grid: 256-row main round + 128-row tail round
 ])
 def test_gemm_headpost_vs_oracle(gpu_device, B, S, nq, nk, nv, K, rope):
     ff = _ff()
@@ -119,3 +120,37 @@ def test_rmsnorm_variants_vs_oracle(gpu_device, D, mod):
     got = outs[0].cpu()
     assert rel_l2(got.float(), ref.float()) < 2e-3
     assert (got != ref).float().mean().item() < 1e-3
+
+
+@pytest.mark.parametrize("B,S,K", [(2, 3000, 2048), (2, 2500, 512), (7, 700, 256)])
+def test_gemm_headpost_tail_split_bit_identical(gpu_device, monkeypatch, B, S, K):
+    """The head-post GEMM as a tail split (whole rounds of 256-row tiles, the remaining rows as
+    one round of 128-row tiles in the same launch, ACEHIP_GEMM_HPTAIL) gives the same bits as
+    the 192-row grid: every output element accumulates the same K-tile MFMAs in the same order,
+    and the tail grid's rows find their (b, s) through HeadPostArgs.m_off."""
+    from conftest import set_knob
+    ff = _ff()
+    nq, nk, nv = 16, 8, 8
+    N = (nq + nk + nv) * 128
+    g = torch.Generator().manual_seed(B * S + K)
+    A = torch.randn(B * S, K, generator=g).bfloat16().to(gpu_device)
+    W = (torch.randn(N, K, generator=g) * 0.05).bfloat16().to(gpu_device)
+    qw = (1 + 0.1 * torch.randn(128, generator=g)).bfloat16().to(gpu_device)
+    kw = (1 + 0.1 * torch.randn(128, generator=g)).bfloat16().to(gpu_device)
+    cos, sin = dit_oracle.rope_tables(S, 128, 1e6, torch.bfloat16)
+    cos, sin = cos[0].contiguous().to(gpu_device), sin[0].contiguous().to(gpu_device)
+
+    def run(tail):
+        set_knob(monkeypatch, "ACEHIP_GEMM_HPTAIL", "1" if tail else "0")
+        out = [torch.full((B, n, S, 128), float("nan"), dtype=torch.bfloat16, device=gpu_device)
+               for n in (nq, nk, nv)]
+        ff.check(ff.lib().acehip_gemm_headpost_bf16(
+            ff.ptr(A), K, ff.ptr(W), K, B, S, nq, nk, nv, ff.ptr(qw), ff.ptr(kw), ff.ptr(cos), ff.ptr(sin), 1e-6,
+            ff.ptr(out[0]), ff.ptr(out[1]), ff.ptr(out[2]), ff.stream_ptr()), "gemm_headpost")
+        torch.cuda.synchronize()
+        return out
+
+    on, off = run(True), run(False)
+    for a, b in zip(on, off):
+        assert torch.isfinite(a.float()).all()
+        assert torch.equal(a, b)
