@@ -1442,7 +1442,7 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
                                                            const bf16_t *__restrict__ v, bf16_t *__restrict__ o, int H,
                                                            int KV, int Sq, int Sk, float sl2, int64_t o_ld, int nparts,
                                                            float *__restrict__ ws, int *__restrict__ cnt,
-                                                           const uint8_t *__restrict__ kmask) {
+                                                           const uint8_t *__restrict__ kmask, int causal) {
     constexpr int VT = KT * 256;                 // one V tile: 64 keys × 256 B
     __shared__ __attribute__((aligned(16))) char lds[4 * 2 * VT];   // 128 KB: per wave two V slots
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1464,7 +1464,9 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
     // attn_fwd_kernel's masked mode — an all-excluded row softmaxes uniformly over its Sk keys
     const uint8_t *km = kmask ? kmask + (int64_t)b * Sk : nullptr;
     // KV part `part` of nparts: tiles [t0, t1); wave w takes t0 + w, t0 + w + 4, …
-    const int ntall = (Sk + KT - 1) / KT, per = (ntall + nparts - 1) / nparts;
+    // causal (the text encoder, no key mask): the unit's keys end at its last row's diagonal
+    const int klast = causal ? min(Sk, min(Sq, qb * 32 + 32)) : Sk;
+    const int ntall = (klast + KT - 1) / KT, per = (ntall + nparts - 1) / nparts;
     const int t0 = min(ntall, part * per), ntiles = min(ntall, t0 + per) - t0;
     const int nmine = ntiles > wave ? (ntiles - wave + 3) / 4 : 0;
     char *const vl = lds + wave * 2 * VT;
@@ -1520,7 +1522,7 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
 #pragma unroll
         for (int s = 0; s < 8; ++s) st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc[8 + s], qf[s], st[1], 0, 0, 0);
         float mx = NEG;
-        if (!km && kv0 + KT <= Sk) {
+        if (!km && kv0 + KT <= Sk && (!causal || kv0 + KT - 1 <= qb * 32)) {
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1531,7 +1533,10 @@ __global__ __launch_bounds__(256, 1) void attn_small_kernel(const bf16_t *__rest
 #pragma unroll
                 for (int jj = 0; jj < 16; ++jj) {
                     const int kj = kv0 + 32 * t + (jj & 3) + 8 * (jj >> 2) + 4 * hh;
-                    const bool inr = kj < Sk;
+                    // keys past the diagonal score NEG like keys past Sk: a wave whose tile is
+                    // wholly past a row's diagonal adds finite garbage that the fold's weight
+                    // 2^(m_w − m) = 0 removes (every row has key 0)
+                    const bool inr = kj < Sk && (!causal || kj <= qi);
                     float sv = inr ? st[t][jj] : NEG;
                     if (km) sv = inr ? (km[kj] != 0 ? sv : NEG) : PAST;   // km is kernel-uniform
                     st[t][jj] = sv;
@@ -1763,7 +1768,8 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
     // S = 750 (768 units) 45.1 / 43.0 vs 34.8 / 34.0 — attn_fwd_kernel's 128-row GQA-pair units
     // read K / V once per pair and tile, and win once the grid fills the chip)
     const int64_t small_units = (int64_t)((Sq + 31) / 32) * H * B;
-    if (kn.attn_small && window < 0 && window != ATTN_CAUSAL && small_units <= cus + cus / 2 &&
+    const bool small_causal = window == ATTN_CAUSAL && !kmask && kn.attn_small_causal;
+    if (kn.attn_small && window < 0 && (window != ATTN_CAUSAL || small_causal) && small_units <= cus + cus / 2 &&
         (!kmask || kn.attn_small_mask)) {
         const int64_t units = small_units;
         // KV parts per unit: about one tile per wave while the grid stays within one round
@@ -1775,7 +1781,7 @@ int attention(const bf16_t *q, const bf16_t *k, const bf16_t *v, bf16_t *o, int 
         attn_small_kernel<<<(unsigned)(units * parts), 256, 0, s>>>(
             q, k, v, o, H, KV, Sq, Sk, sl2, o_ld, parts,
             parts > 1 ? (float *)((char *)ws + (size_t)std::max(1024, cus) * sizeof(int)) : nullptr,
-            parts > 1 ? (int *)ws : nullptr, kmask);
+            parts > 1 ? (int *)ws : nullptr, kmask, small_causal ? 1 : 0);
         HIP_TRY(hipGetLastError());
         return 0;
     }

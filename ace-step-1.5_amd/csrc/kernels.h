@@ -21,6 +21,7 @@ struct Knobs {
     int attn_pw_split = 24;   // ACEHIP_ATTN_PW_SPLIT: shortest KV loop whose tail units are split
     int attn_small = 1;       // ACEHIP_ATTN_SMALL: few-unit unmasked full / cross attention on attn_small_kernel (1 with KV parts, 2 without, 0 off)
     int attn_small_mask = 1;  // ACEHIP_ATTN_SMALL_MASK: key-padding-masked full attention (condition encoders) on attn_small_kernel too
+    int attn_small_causal = 1; // ACEHIP_ATTN_SMALL_CAUSAL: unmasked causal attention (the text encoder) on attn_small_kernel too
     int attn_short_tpp = 3;   // ACEHIP_ATTN_SHORT_TPP: KV tiles per part of the short split
     int attn_cus = 0;         // ACEHIP_ATTN_CUS: CU count the splits plan for (0: the device's)
     int attn_streamk = 1;     // ACEHIP_ATTN_STREAMK: stream-K rounds for unmasked full / cross layers

@@ -32,6 +32,7 @@ Knobs read_env() {
     k.attn_short_tpp = env_int("ACEHIP_ATTN_SHORT_TPP", 3);
     k.attn_small = env_int("ACEHIP_ATTN_SMALL", 1);
     k.attn_small_mask = env_int("ACEHIP_ATTN_SMALL_MASK", 1);
+    k.attn_small_causal = env_int("ACEHIP_ATTN_SMALL_CAUSAL", 1);
     if (k.attn_short_tpp <= 0) k.attn_short_tpp = 3;
     k.attn_cus = env_int("ACEHIP_ATTN_CUS", 0);
     k.attn_streamk = env_int("ACEHIP_ATTN_STREAMK", 1);

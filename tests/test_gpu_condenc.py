@@ -308,3 +308,34 @@ def test_overlapped_text_encoder_feeds_condition_encoder(gpu_device):
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
     ce.close()
+
+
+@pytest.mark.parametrize("B,H,KV,S", [(1, 16, 8, 128), (2, 16, 8, 77), (3, 4, 2, 300), (1, 2, 2, 257)])
+def test_causal_attention_small(gpu_device, monkeypatch, B, H, KV, S):
+    """Unmasked causal attention (the Qwen3 text encoder, 28 layers per song) on attn_small_kernel
+    (ACEHIP_ATTN_SMALL_CAUSAL): each one-head x 32-row unit walks its keys up to its last row's
+    diagonal.  vs fp32 SDPA with is_causal and vs attn_fwd_kernel's causal mode (knob off)."""
+    import math
+    from acehip import _ffi as ff
+    from conftest import rel_l2, set_knob
+    g = torch.Generator().manual_seed(B * 100 + S)
+    q = torch.randn(B, H, S, 128, generator=g).bfloat16().to(gpu_device)
+    k = torch.randn(B, KV, S, 128, generator=g).bfloat16().to(gpu_device)
+    v = torch.randn(B, KV, S, 128, generator=g).bfloat16().to(gpu_device)
+
+    def run(on):
+        set_knob(monkeypatch, "ACEHIP_ATTN_SMALL_CAUSAL", "1" if on else "0")
+        o = torch.full((B, S, H * 128), float("nan"), device=gpu_device, dtype=torch.bfloat16)
+        ff.check(ff.lib().acehip_attention_bf16(ff.ptr(q), ff.ptr(k), ff.ptr(v), ff.ptr(o), B, H, KV, S, S, -2,
+                                                1 / math.sqrt(128), ff.stream_ptr()))
+        torch.cuda.synchronize()
+        return o.float().cpu()
+
+    on, off = run(True), run(False)
+    rep = H // KV
+    ref = torch.nn.functional.scaled_dot_product_attention(
+        q.float(), k.float().repeat_interleave(rep, 1), v.float().repeat_interleave(rep, 1),
+        is_causal=True).transpose(1, 2).reshape(B, S, H * 128).cpu()
+    assert torch.isfinite(on).all()
+    assert rel_l2(on, ref) < 1e-2
+    assert rel_l2(on, off) < 1e-2
